@@ -188,8 +188,8 @@ int nr_sumsq(const float* x, int64_t n, float* acc, nr_stream_t stream);
  * + 1e-6)) when sumsq != NULL (torch.nn.utils.clip_grad_norm_), lr is read
  * from the host (LambdaLR already applied), step is the 1-based Adam step. */
 int nr_adam_step(float* params, float* grads, float* exp_avg,
-                 float* exp_avg_sq, int64_t n, float lr, float beta1,
-                 float beta2, float eps, int64_t step, const float* sumsq,
+                 float* exp_avg_sq, int64_t n, double lr, double beta1,
+                 double beta2, double eps, int64_t step, const float* sumsq,
                  float max_norm, nr_stream_t stream);
 
 /* ---- per-ray glue used by render_rays (rendering.py:119-240) ------------ */

@@ -326,12 +326,14 @@ class CameraPoseParameters(nn.Module):
 
 def get_rays_from_pixels(image_indices, pixel_coords, poses, H, W, focal):
     """Reference noisy_src/data_pose_opt.py:83-148 + :200-223 (poses indexed by image)."""
-    ray_directions = get_ray_directions(H, W, focal).to(pixel_coords.device)
+    ray_directions = get_ray_directions(H, W, focal).to(pixel_coords.device, poses.dtype)
     batch_size = image_indices.shape[0]
     unique_img_indices = torch.unique(image_indices)
     selected = poses[unique_img_indices]
-    rays_o = torch.zeros(batch_size, 3, device=pixel_coords.device)
-    rays_d = torch.zeros(batch_size, 3, device=pixel_coords.device)
+    # reference: torch.zeros(batch_size, 3) (fp32); the dtype follows the poses so the
+    # same restatement can run in fp64 for error studies
+    rays_o = torch.zeros(batch_size, 3, device=pixel_coords.device, dtype=poses.dtype)
+    rays_d = torch.zeros(batch_size, 3, device=pixel_coords.device, dtype=poses.dtype)
     parts = []
     for k, img_idx in enumerate(unique_img_indices):
         mask = image_indices == img_idx
@@ -430,3 +432,26 @@ def compute_pose_error(pose_gt, pose_noisy):
     angle_rad = torch.acos(torch.clamp((trace - 1) / 2, -1, 1))
     return {"rotation_error_deg": float(angle_rad * 180 / math.pi),
             "translation_error": float(torch.norm(pose_gt[:3, 3] - pose_noisy[:3, 3]))}
+
+
+class _Bf16OperandLinear(nn.Module):
+    """nn.Linear whose input and weight are rounded to bf16 (fp32 accumulate, fp32 bias):
+    the operand precision of the MI355X bf16 MFMA path, used as its parity reference."""
+
+    def __init__(self, lin: nn.Linear):
+        super().__init__()
+        self.lin = lin
+
+    def forward(self, x):
+        return F.linear(x.bfloat16().float(), self.lin.weight.bfloat16().float(), self.lin.bias)
+
+
+def bf16_operand_nerf(model: "NeRF") -> "NeRF":
+    """Copy of an oracle NeRF whose MFMA layers (trunk, feature, dir) use bf16 operands."""
+    import copy
+    emu = copy.deepcopy(model)
+    for i in range(len(emu.pts_linears)):
+        emu.pts_linears[i] = _Bf16OperandLinear(emu.pts_linears[i])
+    emu.feature_linear = _Bf16OperandLinear(emu.feature_linear)
+    emu.dir_linear = _Bf16OperandLinear(emu.dir_linear)
+    return emu

@@ -1,0 +1,176 @@
+// Volume-rendering alpha composite (forward + backward) and the MSE loss seed.
+//
+// Reference semantics (ShawnnnLiu/Robust-NeRF):
+//   raw2outputs  noisy_src/rendering.py:20-116
+//   loss         noisy_src/train.py:89,98 (mean((rgb - target)^2))
+// One thread per ray walks its S samples in order, so the transmittance is the
+// same sequential product as torch's CPU cumprod:
+//   delta_i = (z_{i+1} - z_i | 1e10) * |d|;  a_i = 1 - exp(-relu(sigma_i + n_i) * delta_i)
+//   T_0 = 1, T_{i+1} = T_i * (1 - a_i + 1e-10);  w_i = a_i T_i
+//   rgb = sum w c (+ 1 - acc if white), depth = sum w z, acc = sum w.
+// Backward uses the division-free form of torch's cumprod gradient:
+//   dL/da_i = T_i (G_i - R_i),  R_i = G_{i+1} a_{i+1} + t_{i+1} R_{i+1},  R_{S-1} = 0
+// (equal to G_i T_i - (sum_{k>i} G_k w_k) / t_i, the formula autograd evaluates).
+#include "common.hpp"
+
+namespace nr {
+
+struct SampleTerms {
+    float delta_raw, alpha, e, sig;  // sig = relu'd sigma after noise
+};
+
+__device__ __forceinline__ SampleTerms sample_terms(const float* sigma, const float* z, const float* noise,
+                                                    int64_t base, int i, int S, float dnorm) {
+    SampleTerms t;
+    t.delta_raw = i < S - 1 ? z[base + i + 1] - z[base + i] : 1e10f;
+    float s = sigma[base + i];
+    if (noise) s = s + noise[base + i];
+    t.sig = s > 0.f ? s : 0.f;
+    t.e = expf(-t.sig * (t.delta_raw * dnorm));
+    t.alpha = 1.0f - t.e;
+    return t;
+}
+
+__global__ void composite_fwd_kernel(const float* rgb, const float* sigma, const float* z, const float* rd,
+                                     const float* noise, int B, int S, int white, float* rgb_map, float* depth,
+                                     float* acc, float* weights) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const float dnorm = sqrtf(rd[3 * b] * rd[3 * b] + rd[3 * b + 1] * rd[3 * b + 1] + rd[3 * b + 2] * rd[3 * b + 2]);
+    const int64_t base = static_cast<int64_t>(b) * S;
+    float T = 1.0f, r = 0.f, g = 0.f, bl = 0.f, d = 0.f, a = 0.f;
+    for (int i = 0; i < S; ++i) {
+        const SampleTerms st = sample_terms(sigma, z, noise, base, i, S, dnorm);
+        const float w = st.alpha * T;
+        T = T * (1.0f - st.alpha + 1e-10f);
+        if (weights) weights[base + i] = w;
+        const int64_t q = 3 * (base + i);
+        r += w * rgb[q];
+        g += w * rgb[q + 1];
+        bl += w * rgb[q + 2];
+        d += w * z[base + i];
+        a += w;
+    }
+    if (white) {
+        r = r + (1.0f - a);
+        g = g + (1.0f - a);
+        bl = bl + (1.0f - a);
+    }
+    rgb_map[3 * b] = r;
+    rgb_map[3 * b + 1] = g;
+    rgb_map[3 * b + 2] = bl;
+    if (depth) depth[b] = d;
+    if (acc) acc[b] = a;
+}
+
+// g_sigma doubles as scratch for T_i between the two passes.
+__global__ void composite_bwd_kernel(const float* rgb, const float* sigma, const float* z, const float* rd,
+                                     const float* noise, int B, int S, int white, const float* g_map,
+                                     const float* g_depth, const float* g_acc, const float* g_w, float* g_rgb,
+                                     float* g_sigma, float* g_rd) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const float dx = rd[3 * b], dy = rd[3 * b + 1], dz = rd[3 * b + 2];
+    const float dnorm = sqrtf(dx * dx + dy * dy + dz * dz);
+    const int64_t base = static_cast<int64_t>(b) * S;
+    const float gr = g_map[3 * b], gg = g_map[3 * b + 1], gb = g_map[3 * b + 2];
+    const float gd = g_depth ? g_depth[b] : 0.f;
+    const float ga = (g_acc ? g_acc[b] : 0.f) - (white ? (gr + gg) + gb : 0.f);
+    // pass 1: transmittance T_i -> g_sigma scratch
+    float T = 1.0f;
+    for (int i = 0; i < S; ++i) {
+        const SampleTerms st = sample_terms(sigma, z, noise, base, i, S, dnorm);
+        g_sigma[base + i] = T;
+        T = T * (1.0f - st.alpha + 1e-10f);
+    }
+    // pass 2: reverse recurrence
+    float R = 0.f, Gn = 0.f, an = 0.f, tn = 0.f, g_norm = 0.f;
+    for (int i = S - 1; i >= 0; --i) {
+        const SampleTerms st = sample_terms(sigma, z, noise, base, i, S, dnorm);
+        const int64_t q = 3 * (base + i);
+        const float Ti = g_sigma[base + i];
+        const float w = st.alpha * Ti;
+        const float c0 = rgb[q], c1 = rgb[q + 1], c2 = rgb[q + 2];
+        float G = ((gr * c0 + gg * c1) + gb * c2) + gd * z[base + i] + ga;
+        if (g_w) G += g_w[base + i];
+        g_rgb[q] = gr * w;
+        g_rgb[q + 1] = gg * w;
+        g_rgb[q + 2] = gb * w;
+        if (i < S - 1) R = Gn * an + tn * R;
+        const float g_alpha = Ti * (G - R);
+        // alpha = 1 - exp(x), x = -relu(s) * delta_raw * |d|
+        const float g_x = -g_alpha * st.e;
+        const float delta = st.delta_raw * dnorm;
+        g_sigma[base + i] = (st.sig > 0.f) ? -g_x * delta : 0.f;
+        g_norm += g_x * (-st.sig * st.delta_raw);
+        Gn = G;
+        an = st.alpha;
+        tn = 1.0f - st.alpha + 1e-10f;
+    }
+    if (g_rd) {
+        g_rd[3 * b] += g_norm * dx / dnorm;
+        g_rd[3 * b + 1] += g_norm * dy / dnorm;
+        g_rd[3 * b + 2] += g_norm * dz / dnorm;
+    }
+}
+
+// loss = mean((p - t)^2) over n = 3B; g = 2 (p - t) / n * scale.  One block.
+__global__ void mse_kernel(const float* p, const float* t, int n, float scale, float* loss, float* g) {
+    __shared__ float part[16];
+    float s = 0.f;
+    const float inv = 1.0f / static_cast<float>(n);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const float d = p[i] - t[i];
+        s += d * d;
+        if (g) g[i] = (2.0f * d) * inv * scale;
+    }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) part[w] = s;
+    __syncthreads();
+    if (threadIdx.x == 0 && loss) {
+        float tot = 0.f;
+        for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) tot += part[i];
+        *loss = tot * inv;
+    }
+}
+
+}  // namespace nr
+
+using namespace nr;
+
+extern "C" {
+
+int nr_composite_fwd(const float* rgb, const float* sigma, const float* z, const float* rd, const float* noise, int B,
+                     int S, int white, float* rgb_map, float* depth, float* acc, float* weights,
+                     nr_stream_t stream) {
+    NR_REQUIRE(rgb && sigma && z && rd && rgb_map && B >= 0 && S > 0, "nr_composite_fwd: bad arguments");
+    if (B == 0) return NR_OK;
+    hipLaunchKernelGGL(composite_fwd_kernel, dim3(ceil_div(B, 64)), dim3(64), 0, static_cast<hipStream_t>(stream),
+                       rgb, sigma, z, rd, noise, B, S, white, rgb_map, depth, acc, weights);
+    NR_LAUNCH_CHECK("nr_composite_fwd");
+    return NR_OK;
+}
+
+int nr_composite_bwd(const float* rgb, const float* sigma, const float* z, const float* rd, const float* noise, int B,
+                     int S, int white, const float* g_map, const float* g_depth, const float* g_acc,
+                     const float* g_w, float* g_rgb, float* g_sigma, float* g_rd, nr_stream_t stream) {
+    NR_REQUIRE(rgb && sigma && z && rd && g_map && g_rgb && g_sigma && B >= 0 && S > 0,
+               "nr_composite_bwd: bad arguments");
+    if (B == 0) return NR_OK;
+    hipLaunchKernelGGL(composite_bwd_kernel, dim3(ceil_div(B, 64)), dim3(64), 0, static_cast<hipStream_t>(stream),
+                       rgb, sigma, z, rd, noise, B, S, white, g_map, g_depth, g_acc, g_w, g_rgb, g_sigma, g_rd);
+    NR_LAUNCH_CHECK("nr_composite_bwd");
+    return NR_OK;
+}
+
+int nr_mse_fwd_bwd(const float* pred, const float* target, int B, float scale, float* loss, float* g,
+                   nr_stream_t stream) {
+    NR_REQUIRE(pred && target && B > 0, "nr_mse_fwd_bwd: bad arguments");
+    hipLaunchKernelGGL(mse_kernel, dim3(1), dim3(1024), 0, static_cast<hipStream_t>(stream), pred, target, 3 * B,
+                       scale, loss, g);
+    NR_LAUNCH_CHECK("nr_mse_fwd_bwd");
+    return NR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,113 @@
+// Optimizer tail: global-norm gradient clipping and Adam on flat fp32 buffers.
+//
+// Reference semantics (ShawnnnLiu/Robust-NeRF):
+//   torch.nn.utils.clip_grad_norm_(params, max_norm)  noisy_src/train.py:115,
+//       noisy_src/train_pose_opt.py:398-404: coef = min(1, max_norm / (||g||_2 + 1e-6))
+//   torch.optim.Adam(lr, betas=(0.9, 0.999), eps=1e-8)  noisy_src/train.py:402
+//       m.lerp_(g, 1-b1); v = b2 v + (1-b2) g^2; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
+//   LambdaLR 0.1^(step/250000)                          noisy_src/train.py:405-411 (host)
+// HBM-bound: ~20 B read + 16 B written per parameter; 16-B vector accesses.
+#include <cmath>
+
+#include "common.hpp"
+
+namespace nr {
+
+__global__ void sumsq_kernel(const float* x, int64_t n, float* acc) {
+    float s = 0.f;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    const int64_t n4 = n / 4;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const float4 v = x4[i];
+        s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    for (int64_t i = 4 * n4 + static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+        s += x[i] * x[i];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    __shared__ float part[16];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) t += part[i];
+        atomicAdd(acc, t);
+    }
+}
+
+__device__ __forceinline__ void adam_one(float& p, float& g, float& m, float& v, float coef, float omb1, float b2,
+                                         float omb2, float step_size, float bc2_sqrt, float eps) {
+    g = g * coef;
+    m = m + omb1 * (g - m);  // exp_avg.lerp_(grad, 1 - beta1)
+    v = v * b2 + (omb2 * g) * g;  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p = p - step_size * (m / denom);
+}
+
+__global__ void adam_kernel(float* p, float* g, float* m, float* v, int64_t n, float omb1, float b2, float omb2,
+                            float eps,
+                            float step_size, float bc2_sqrt, const float* sumsq, float max_norm) {
+    float coef = 1.0f;
+    if (sumsq) {
+        const float total = sqrtf(*sumsq);
+        const float c = max_norm / (total + 1e-6f);
+        coef = c < 1.0f ? c : 1.0f;
+    }
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    const int64_t n4 = n / 4;
+    float4* p4 = reinterpret_cast<float4*>(p);
+    float4* g4 = reinterpret_cast<float4*>(g);
+    float4* m4 = reinterpret_cast<float4*>(m);
+    float4* v4 = reinterpret_cast<float4*>(v);
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 P = p4[i], G = g4[i], M = m4[i], V = v4[i];
+        adam_one(P.x, G.x, M.x, V.x, coef, omb1, b2, omb2, step_size, bc2_sqrt, eps);
+        adam_one(P.y, G.y, M.y, V.y, coef, omb1, b2, omb2, step_size, bc2_sqrt, eps);
+        adam_one(P.z, G.z, M.z, V.z, coef, omb1, b2, omb2, step_size, bc2_sqrt, eps);
+        adam_one(P.w, G.w, M.w, V.w, coef, omb1, b2, omb2, step_size, bc2_sqrt, eps);
+        p4[i] = P;
+        g4[i] = G;
+        m4[i] = M;
+        v4[i] = V;
+    }
+    for (int64_t i = 4 * n4 + static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+        adam_one(p[i], g[i], m[i], v[i], coef, omb1, b2, omb2, step_size, bc2_sqrt, eps);
+}
+
+}  // namespace nr
+
+using namespace nr;
+
+extern "C" {
+
+int nr_sumsq(const float* x, int64_t n, float* acc, nr_stream_t stream) {
+    NR_REQUIRE(x && acc && n >= 0, "nr_sumsq: bad arguments");
+    NR_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0, "nr_sumsq: x must be 16-byte aligned");
+    if (n == 0) return NR_OK;
+    const int grid = stream_grid(ceil_div_ll(n, 4), 256) > 512 ? 512 : stream_grid(ceil_div_ll(n, 4), 256);
+    hipLaunchKernelGGL(sumsq_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), x, n, acc);
+    NR_LAUNCH_CHECK("nr_sumsq");
+    return NR_OK;
+}
+
+int nr_adam_step(float* p, float* g, float* m, float* v, int64_t n, double lr, double b1, double b2, double eps,
+                 int64_t step, const float* sumsq, float max_norm, nr_stream_t stream) {
+    NR_REQUIRE(p && g && m && v && n >= 0 && step >= 1, "nr_adam_step: bad arguments");
+    NR_REQUIRE(((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+                 reinterpret_cast<uintptr_t>(v)) & 15) == 0,
+               "nr_adam_step: buffers must be 16-byte aligned");
+    if (n == 0) return NR_OK;
+    // bias corrections in double on the host, as torch's _single/_multi_tensor_adam do
+    const double bc1 = 1.0 - std::pow(b1, static_cast<double>(step));
+    const double bc2 = 1.0 - std::pow(b2, static_cast<double>(step));
+    const float step_size = static_cast<float>(lr / bc1);
+    const float bc2_sqrt = static_cast<float>(std::sqrt(bc2));
+    const int grid = stream_grid(ceil_div_ll(n, 4), 256);
+    hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), p, g, m, v, n,
+                       static_cast<float>(1.0 - b1), static_cast<float>(b2), static_cast<float>(1.0 - b2),
+                       static_cast<float>(eps), step_size, bc2_sqrt, sumsq, max_norm);
+    NR_LAUNCH_CHECK("nr_adam_step");
+    return NR_OK;
+}
+
+}  // extern "C"

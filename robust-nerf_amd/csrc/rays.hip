@@ -1,0 +1,500 @@
+// Ray generation, SE(3) camera poses, stratified sampling and positional
+// encoding: the per-ray / per-sample elementwise part of the hot path.
+//
+// Reference semantics (ShawnnnLiu/Robust-NeRF):
+//   get_ray_directions  noisy_src/rays.py:17-64
+//   get_rays            noisy_src/rays.py:67-99
+//   get_rays_from_pixels noisy_src/data_pose_opt.py:83-148, :200-223
+//   CameraPoseParameters noisy_src/train_pose_opt.py:122-226
+//   sample_along_rays   noisy_src/rays.py:145-210
+//   PositionalEncoding  noisy_src/model.py:20-80
+// The library is built with -ffp-contract=off so that each a*b+c rounds twice,
+// exactly as the reference's separate eager torch ops do.
+#include "common.hpp"
+
+namespace nr {
+
+// torch.linspace(start, end, n)[i] (aten/native/cpu + cuda RangeFactories: symmetric form).
+__device__ __forceinline__ float linspace_at(float start, float end, int n, int i) {
+    if (n == 1) return start;
+    const float step = (end - start) / static_cast<float>(n - 1);
+    const int halfway = n / 2;
+    return i < halfway ? start + step * static_cast<float>(i)
+                       : end - step * static_cast<float>(n - 1 - i);
+}
+
+__device__ __forceinline__ float norm3(float x, float y, float z) {
+    return sqrtf(x * x + y * y + z * z);
+}
+
+// ---------------------------------------------------------------- A1 -----
+__global__ void ray_directions_kernel(int H, int W, float focal, float cx, float cy, float* dirs) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= H * W) return;
+    const int j = p / W, i = p % W;  // meshgrid indexing='xy': dirs[j][i]
+    dirs[3 * p + 0] = (static_cast<float>(i) - cx) / focal;
+    dirs[3 * p + 1] = -((static_cast<float>(j) - cy) / focal);
+    dirs[3 * p + 2] = -1.0f;
+}
+
+// rays_d = normalize(sum_k dir[k] * R[:,k]) (rays.py:89-94), rays_o = t.
+__device__ __forceinline__ void rotate_normalize(const float* R /*4x4 row-major*/, float dx, float dy,
+                                                 float dz, float& ox, float& oy, float& oz) {
+    const float vx = (dx * R[0] + dy * R[1]) + dz * R[2];
+    const float vy = (dx * R[4] + dy * R[5]) + dz * R[6];
+    const float vz = (dx * R[8] + dy * R[9]) + dz * R[10];
+    const float n = norm3(vx, vy, vz);
+    ox = vx / n;
+    oy = vy / n;
+    oz = vz / n;
+}
+
+// ---------------------------------------------------------------- A2 -----
+__global__ void get_rays_kernel(const float* dirs, const float* c2w, int64_t N, float* ro, float* rd) {
+    const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (p >= N) return;
+    float x, y, z;
+    rotate_normalize(c2w, dirs[3 * p], dirs[3 * p + 1], dirs[3 * p + 2], x, y, z);
+    rd[3 * p] = x;
+    rd[3 * p + 1] = y;
+    rd[3 * p + 2] = z;
+    ro[3 * p] = c2w[3];
+    ro[3 * p + 1] = c2w[7];
+    ro[3 * p + 2] = c2w[11];
+}
+
+// ---------------------------------------------------------------- A3 -----
+// Camera-frame direction of pixel (u,v): the reference gathers it from the
+// precomputed get_ray_directions table with .long() (truncating) indices.
+__device__ __forceinline__ void pixel_dir(const float* pix, int b, int W, int H, float focal, float& dx,
+                                          float& dy) {
+    const int u = static_cast<int>(pix[2 * b]);
+    const int v = static_cast<int>(pix[2 * b + 1]);
+    dx = (static_cast<float>(u) - static_cast<float>(W) * 0.5f) / focal;
+    dy = -((static_cast<float>(v) - static_cast<float>(H) * 0.5f) / focal);
+}
+
+__global__ void rays_from_pixels_fwd_kernel(const int64_t* img_idx, const float* pix, const float* poses,
+                                            int n_img, int H, int W, float focal, int B, float* ro,
+                                            float* rd) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int64_t img = img_idx[b];
+    if (img < 0 || img >= n_img) {  // out-of-range image index: poison the ray, never read out of bounds
+        for (int c = 0; c < 3; ++c) ro[3 * b + c] = rd[3 * b + c] = __builtin_nanf("");
+        return;
+    }
+    const float* P = poses + 16 * img;
+    float dx, dy;
+    pixel_dir(pix, b, W, H, focal, dx, dy);
+    float x, y, z;
+    rotate_normalize(P, dx, dy, -1.0f, x, y, z);
+    rd[3 * b] = x;
+    rd[3 * b + 1] = y;
+    rd[3 * b + 2] = z;
+    ro[3 * b] = P[3];
+    ro[3 * b + 1] = P[7];
+    ro[3 * b + 2] = P[11];
+}
+
+__global__ void rays_from_pixels_bwd_kernel(const int64_t* img_idx, const float* pix, const float* poses,
+                                            int n_img, int H, int W, float focal, int B,
+                                            const float* g_ro, const float* g_rd, float* g_poses) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int64_t img = img_idx[b];
+    if (img < 0 || img >= n_img) return;
+    float* G = g_poses + 16 * img;
+    atomicAdd(G + 3, g_ro[3 * b]);
+    atomicAdd(G + 7, g_ro[3 * b + 1]);
+    atomicAdd(G + 11, g_ro[3 * b + 2]);
+    if (g_rd == nullptr) return;
+    const float* P = poses + 16 * img;
+    float dx, dy;
+    pixel_dir(pix, b, W, H, focal, dx, dy);
+    const float dz = -1.0f;
+    const float vx = (dx * P[0] + dy * P[1]) + dz * P[2];
+    const float vy = (dx * P[4] + dy * P[5]) + dz * P[6];
+    const float vz = (dx * P[8] + dy * P[9]) + dz * P[10];
+    const float n = norm3(vx, vy, vz);
+    const float ux = vx / n, uy = vy / n, uz = vz / n;
+    const float gx = g_rd[3 * b], gy = g_rd[3 * b + 1], gz = g_rd[3 * b + 2];
+    const float dot = ux * gx + uy * gy + uz * gz;
+    const float gvx = (gx - ux * dot) / n, gvy = (gy - uy * dot) / n, gvz = (gz - uz * dot) / n;
+    const float d3[3] = {dx, dy, dz};
+    const float gv[3] = {gvx, gvy, gvz};
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) atomicAdd(G + 4 * r + k, gv[r] * d3[k]);
+}
+
+// ---------------------------------------------------------------- A4 -----
+// Rodrigues with the reference's small-angle rule (train_pose_opt.py:136-163).
+__device__ void rodrigues(const float w[3], float R[9], bool& small) {
+    const float ang = norm3(w[0], w[1], w[2]);
+    small = ang < 1e-6f;
+    const float a = small ? 1.0f : ang;
+    const float k0 = w[0] / a, k1 = w[1] / a, k2 = w[2] / a;
+    // K = skew(axis); K2 = K @ K
+    const float K[9] = {0.f, -k2, k1, k2, 0.f, -k0, -k1, k0, 0.f};
+    float K2[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+            K2[3 * r + c] = (K[3 * r] * K[c] + K[3 * r + 1] * K[3 + c]) + K[3 * r + 2] * K[6 + c];
+    const float s = sinf(a), cc = 1.0f - cosf(a);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            const float I = (r == c) ? 1.0f : 0.0f;
+            R[3 * r + c] = small ? I : (I + s * K[3 * r + c]) + cc * K2[3 * r + c];
+        }
+}
+
+__global__ void se3_poses_fwd_kernel(const float* init, const float* rot, const float* trans,
+                                     const int64_t* indices, int n, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t idx = indices ? indices[i] : i;
+    const float* P = init + 16 * idx;
+    float* O = out + 16 * i;
+    float Rn[9];
+    if (rot) {
+        const float w[3] = {rot[3 * idx], rot[3 * idx + 1], rot[3 * idx + 2]};
+        float Rd[9];
+        bool small;
+        rodrigues(w, Rd, small);
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c)
+                Rn[3 * r + c] = (Rd[3 * r] * P[c] + Rd[3 * r + 1] * P[4 + c]) + Rd[3 * r + 2] * P[8 + c];
+    } else {
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) Rn[3 * r + c] = P[4 * r + c];
+    }
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) O[4 * r + c] = Rn[3 * r + c];
+        O[4 * r + 3] = trans ? P[4 * r + 3] + trans[3 * idx + r] : P[4 * r + 3];
+    }
+    O[12] = 0.f;
+    O[13] = 0.f;
+    O[14] = 0.f;
+    O[15] = 1.f;
+}
+
+__global__ void se3_poses_bwd_kernel(const float* init, const float* rot, const int64_t* indices, int n,
+                                     const float* g_poses, int fixed_small, float* g_rot, float* g_trans) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t idx = indices ? indices[i] : i;
+    const float* G = g_poses + 16 * i;
+    if (g_trans)
+        for (int r = 0; r < 3; ++r) atomicAdd(g_trans + 3 * idx + r, G[4 * r + 3]);
+    if (!g_rot || !rot) return;
+    const float* P = init + 16 * idx;
+    // g_Rdelta = g_Rnew @ R_init^T
+    float gRd[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+            gRd[3 * r + c] = (G[4 * r] * P[4 * c] + G[4 * r + 1] * P[4 * c + 1]) + G[4 * r + 2] * P[4 * c + 2];
+    const float w[3] = {rot[3 * idx], rot[3 * idx + 1], rot[3 * idx + 2]};
+    const float th = norm3(w[0], w[1], w[2]);
+    float gw[3] = {0.f, 0.f, 0.f};
+    // skew(e_m) entries: E_m[r][c]
+    auto E = [](int m, int r, int c) -> float {
+        // skew(v) = [[0,-v2,v1],[v2,0,-v0],[-v1,v0,0]]
+        const int id = 3 * r + c;
+        if (m == 0) return id == 5 ? -1.f : (id == 7 ? 1.f : 0.f);
+        if (m == 1) return id == 2 ? 1.f : (id == 6 ? -1.f : 0.f);
+        return id == 1 ? -1.f : (id == 3 ? 1.f : 0.f);
+    };
+    if (th < 1e-6f) {
+        // Reference: torch.where(small, I, R) -> exactly zero gradient (train_pose_opt.py:143-161).
+        if (fixed_small)
+            for (int m = 0; m < 3; ++m) {
+                float s = 0.f;
+                for (int e = 0; e < 9; ++e) s += gRd[e] * E(m, e / 3, e % 3);
+                gw[m] = s;
+            }
+    } else {
+        const float a[3] = {w[0] / th, w[1] / th, w[2] / th};
+        const float K[9] = {0.f, -a[2], a[1], a[2], 0.f, -a[0], -a[1], a[0], 0.f};
+        float K2[9];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c)
+                K2[3 * r + c] = K[3 * r] * K[c] + K[3 * r + 1] * K[3 + c] + K[3 * r + 2] * K[6 + c];
+        const float s = sinf(th), cs = cosf(th), cc = 1.f - cs;
+        float g_th = 0.f;
+        for (int e = 0; e < 9; ++e) g_th += gRd[e] * (cs * K[e] + s * K2[e]);
+        float ga[3];
+        for (int m = 0; m < 3; ++m) {
+            float acc = 0.f;
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) {
+                    float EK = 0.f, KE = 0.f;
+                    for (int q = 0; q < 3; ++q) {
+                        EK += E(m, r, q) * K[3 * q + c];
+                        KE += K[3 * r + q] * E(m, q, c);
+                    }
+                    acc += gRd[3 * r + c] * (s * E(m, r, c) + cc * (EK + KE));
+                }
+            ga[m] = acc;
+        }
+        const float adg = a[0] * ga[0] + a[1] * ga[1] + a[2] * ga[2];
+        for (int m = 0; m < 3; ++m) gw[m] = g_th * a[m] + (ga[m] - a[m] * adg) / th;
+    }
+    for (int m = 0; m < 3; ++m) atomicAdd(g_rot + 3 * idx + m, gw[m]);
+}
+
+// ---------------------------------------------------------------- A5 -----
+__global__ void stratified_kernel(const float* ro, const float* rd, const float* t_rand, float near_,
+                                  float far_, int lindisp, int B, int N, float* z_out, float* pts) {
+    const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (p >= static_cast<int64_t>(B) * N) return;
+    const int b = static_cast<int>(p / N), i = static_cast<int>(p % N);
+    auto zlin = [&](int k) -> float {
+        const float t = linspace_at(0.f, 1.f, N, k);
+        if (lindisp) return 1.0f / ((1.0f / near_) * (1.0f - t) + (1.0f / far_) * t);
+        return near_ * (1.0f - t) + far_ * t;
+    };
+    float z = zlin(i);
+    if (t_rand) {
+        const float zp = i > 0 ? zlin(i - 1) : 0.f;
+        const float zn = i < N - 1 ? zlin(i + 1) : 0.f;
+        const float lower = i > 0 ? 0.5f * (z + zp) : z;      // cat([z[:1], mids])
+        const float upper = i < N - 1 ? 0.5f * (zn + z) : z;  // cat([mids, z[-1:]])
+        z = lower + (upper - lower) * t_rand[p];
+    }
+    z_out[p] = z;
+    if (pts) {
+        for (int c = 0; c < 3; ++c) pts[3 * p + c] = ro[3 * b + c] + rd[3 * b + c] * z;
+    }
+}
+
+// ---------------------------------------------------------------- A6 -----
+__device__ __forceinline__ float pe_freq(int k, int L, int log_sampling) {
+    if (log_sampling) return exp2f(linspace_at(0.f, static_cast<float>(L - 1), L, k));
+    return linspace_at(1.f, exp2f(static_cast<float>(L - 1)), L, k);
+}
+
+__global__ void pe_kernel(const float* x, int64_t M, int C, int L, int inc, int logs, float* out) {
+    const int D = inc + 2 * L;
+    const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (p >= M * C * D) return;
+    const int64_t m = p / (C * D);
+    const int col = static_cast<int>(p % (C * D));
+    const int blk = col / C, c = col % C;  // output block blk of width C
+    const float v = x[m * C + c];
+    float r;
+    if (inc && blk == 0) {
+        r = v;
+    } else {
+        const int q = blk - inc;
+        const float f = pe_freq(q >> 1, L, logs);
+        r = (q & 1) ? cosf(f * v) : sinf(f * v);
+    }
+    out[p] = r;
+}
+
+__global__ void pe_bwd_kernel(const float* x, int64_t M, int C, int L, int inc, int logs, const float* g,
+                              float* gx) {
+    const int D = inc + 2 * L;
+    const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (p >= M * C) return;
+    const int64_t m = p / C;
+    const int c = static_cast<int>(p % C);
+    const float v = x[p];
+    const float* gr = g + m * C * D;
+    float acc = inc ? gr[c] : 0.f;
+    for (int k = 0; k < L; ++k) {
+        const float f = pe_freq(k, L, logs);
+        const float a = f * v;
+        acc += gr[(inc + 2 * k) * C + c] * (cosf(a) * f);
+        acc += gr[(inc + 2 * k + 1) * C + c] * (-sinf(a) * f);
+    }
+    gx[p] = acc;
+}
+
+// ---------------------------------------------------------------- glue ----
+__global__ void expand_viewdirs_kernel(const float* rd, int B, int S, float* out) {
+    const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (p >= static_cast<int64_t>(B) * S) return;
+    const int b = static_cast<int>(p / S);
+    const float x = rd[3 * b], y = rd[3 * b + 1], z = rd[3 * b + 2];
+    const float n = norm3(x, y, z);
+    out[3 * p] = x / n;
+    out[3 * p + 1] = y / n;
+    out[3 * p + 2] = z / n;
+}
+
+// One wave per ray: sum over its S samples.
+__global__ void pts_bwd_kernel(const float* g_pts, const float* z, int B, int S, float* g_ro, float* g_rd) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (b >= B) return;
+    float so[3] = {0.f, 0.f, 0.f}, sd[3] = {0.f, 0.f, 0.f};
+    for (int s = lane; s < S; s += 64) {
+        const int64_t q = static_cast<int64_t>(b) * S + s;
+        const float zz = z[q];
+        for (int c = 0; c < 3; ++c) {
+            const float g = g_pts[3 * q + c];
+            so[c] += g;
+            sd[c] += g * zz;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1)
+        for (int c = 0; c < 3; ++c) {
+            so[c] += __shfl_xor(so[c], off);
+            sd[c] += __shfl_xor(sd[c], off);
+        }
+    if (lane == 0)
+        for (int c = 0; c < 3; ++c) {
+            if (g_ro) g_ro[3 * b + c] += so[c];
+            if (g_rd) g_rd[3 * b + c] += sd[c];
+        }
+}
+
+__global__ void viewdirs_bwd_kernel(const float* rd, const float* g_vd, int B, int S, float* g_rd) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (b >= B) return;
+    float sg[3] = {0.f, 0.f, 0.f};
+    for (int s = lane; s < S; s += 64) {
+        const int64_t q = static_cast<int64_t>(b) * S + s;
+        for (int c = 0; c < 3; ++c) sg[c] += g_vd[3 * q + c];
+    }
+    for (int off = 32; off > 0; off >>= 1)
+        for (int c = 0; c < 3; ++c) sg[c] += __shfl_xor(sg[c], off);
+    if (lane == 0) {
+        const float x = rd[3 * b], y = rd[3 * b + 1], z = rd[3 * b + 2];
+        const float n = norm3(x, y, z);
+        const float u[3] = {x / n, y / n, z / n};
+        const float dot = u[0] * sg[0] + u[1] * sg[1] + u[2] * sg[2];
+        for (int c = 0; c < 3; ++c) g_rd[3 * b + c] += (sg[c] - u[c] * dot) / n;
+    }
+}
+
+}  // namespace nr
+
+using namespace nr;
+
+extern "C" {
+
+int nr_ray_directions(int H, int W, float focal, float cx, float cy, float* dirs, nr_stream_t stream) {
+    NR_REQUIRE(H > 0 && W > 0 && dirs, "nr_ray_directions: bad arguments");
+    const int n = H * W;
+    hipLaunchKernelGGL(ray_directions_kernel, dim3(ceil_div(n, 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), H, W, focal, cx, cy, dirs);
+    NR_LAUNCH_CHECK("nr_ray_directions");
+    return NR_OK;
+}
+
+int nr_get_rays(const float* dirs, const float* c2w, int64_t N, float* ro, float* rd, nr_stream_t stream) {
+    NR_REQUIRE(dirs && c2w && ro && rd && N >= 0, "nr_get_rays: bad arguments");
+    if (N == 0) return NR_OK;
+    hipLaunchKernelGGL(get_rays_kernel, dim3(static_cast<unsigned>(ceil_div_ll(N, 256))), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), dirs, c2w, N, ro, rd);
+    NR_LAUNCH_CHECK("nr_get_rays");
+    return NR_OK;
+}
+
+int nr_rays_from_pixels_fwd(const int64_t* img_idx, const float* pix, const float* poses, int n_img, int H,
+                            int W, float focal, int B, float* ro, float* rd, nr_stream_t stream) {
+    NR_REQUIRE(img_idx && pix && poses && ro && rd && B >= 0 && n_img > 0, "nr_rays_from_pixels_fwd: bad arguments");
+    if (B == 0) return NR_OK;
+    hipLaunchKernelGGL(rays_from_pixels_fwd_kernel, dim3(ceil_div(B, 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), img_idx, pix, poses, n_img, H, W, focal, B, ro, rd);
+    NR_LAUNCH_CHECK("nr_rays_from_pixels_fwd");
+    return NR_OK;
+}
+
+int nr_rays_from_pixels_bwd(const int64_t* img_idx, const float* pix, const float* poses, int n_img, int H,
+                            int W, float focal, int B, const float* g_ro, const float* g_rd, float* g_poses,
+                            nr_stream_t stream) {
+    NR_REQUIRE(img_idx && pix && poses && g_ro && g_poses && B >= 0, "nr_rays_from_pixels_bwd: bad arguments");
+    if (B == 0) return NR_OK;
+    hipLaunchKernelGGL(rays_from_pixels_bwd_kernel, dim3(ceil_div(B, 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), img_idx, pix, poses, n_img, H, W, focal, B, g_ro, g_rd,
+                       g_poses);
+    NR_LAUNCH_CHECK("nr_rays_from_pixels_bwd");
+    return NR_OK;
+}
+
+int nr_se3_poses_fwd(const float* init, const float* rot, const float* trans, const int64_t* indices, int n,
+                     float* out, nr_stream_t stream) {
+    NR_REQUIRE(init && out && n >= 0, "nr_se3_poses_fwd: bad arguments");
+    if (n == 0) return NR_OK;
+    hipLaunchKernelGGL(se3_poses_fwd_kernel, dim3(ceil_div(n, 64)), dim3(64), 0, static_cast<hipStream_t>(stream),
+                       init, rot, trans, indices, n, out);
+    NR_LAUNCH_CHECK("nr_se3_poses_fwd");
+    return NR_OK;
+}
+
+int nr_se3_poses_bwd(const float* init, const float* rot, const int64_t* indices, int n, const float* g_poses,
+                     int fixed_small, float* g_rot, float* g_trans, nr_stream_t stream) {
+    NR_REQUIRE(init && g_poses && n >= 0, "nr_se3_poses_bwd: bad arguments");
+    if (n == 0) return NR_OK;
+    hipLaunchKernelGGL(se3_poses_bwd_kernel, dim3(ceil_div(n, 64)), dim3(64), 0, static_cast<hipStream_t>(stream),
+                       init, rot, indices, n, g_poses, fixed_small, g_rot, g_trans);
+    NR_LAUNCH_CHECK("nr_se3_poses_bwd");
+    return NR_OK;
+}
+
+int nr_stratified_sample(const float* ro, const float* rd, const float* t_rand, float near_, float far_,
+                         int lindisp, int B, int N, float* z, float* pts, nr_stream_t stream) {
+    NR_REQUIRE(z && B >= 0 && N > 0 && (!pts || (ro && rd)), "nr_stratified_sample: bad arguments");
+    const int64_t n = static_cast<int64_t>(B) * N;
+    if (n == 0) return NR_OK;
+    hipLaunchKernelGGL(stratified_kernel, dim3(static_cast<unsigned>(ceil_div_ll(n, 256))), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), ro, rd, t_rand, near_, far_, lindisp, B, N, z, pts);
+    NR_LAUNCH_CHECK("nr_stratified_sample");
+    return NR_OK;
+}
+
+int nr_positional_encoding(const float* x, int64_t M, int C, int L, int inc, int logs, float* out,
+                           nr_stream_t stream) {
+    NR_REQUIRE(x && out && M >= 0 && C > 0 && L >= 0, "nr_positional_encoding: bad arguments");
+    const int64_t n = M * C * (inc + 2 * L);
+    if (n == 0) return NR_OK;
+    hipLaunchKernelGGL(pe_kernel, dim3(static_cast<unsigned>(ceil_div_ll(n, 256))), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), x, M, C, L, inc, logs, out);
+    NR_LAUNCH_CHECK("nr_positional_encoding");
+    return NR_OK;
+}
+
+int nr_positional_encoding_bwd(const float* x, int64_t M, int C, int L, int inc, int logs, const float* g,
+                               float* gx, nr_stream_t stream) {
+    NR_REQUIRE(x && g && gx && M >= 0 && C > 0 && L >= 0, "nr_positional_encoding_bwd: bad arguments");
+    const int64_t n = M * C;
+    if (n == 0) return NR_OK;
+    hipLaunchKernelGGL(pe_bwd_kernel, dim3(static_cast<unsigned>(ceil_div_ll(n, 256))), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), x, M, C, L, inc, logs, g, gx);
+    NR_LAUNCH_CHECK("nr_positional_encoding_bwd");
+    return NR_OK;
+}
+
+int nr_expand_viewdirs(const float* rd, int B, int S, float* out, nr_stream_t stream) {
+    NR_REQUIRE(rd && out && B >= 0 && S > 0, "nr_expand_viewdirs: bad arguments");
+    const int64_t n = static_cast<int64_t>(B) * S;
+    if (n == 0) return NR_OK;
+    hipLaunchKernelGGL(expand_viewdirs_kernel, dim3(static_cast<unsigned>(ceil_div_ll(n, 256))), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), rd, B, S, out);
+    NR_LAUNCH_CHECK("nr_expand_viewdirs");
+    return NR_OK;
+}
+
+int nr_pts_bwd(const float* g_pts, const float* z, int B, int S, float* g_ro, float* g_rd, nr_stream_t stream) {
+    NR_REQUIRE(g_pts && z && B >= 0 && S > 0, "nr_pts_bwd: bad arguments");
+    if (B == 0 || (!g_ro && !g_rd)) return NR_OK;
+    hipLaunchKernelGGL(pts_bwd_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, static_cast<hipStream_t>(stream), g_pts,
+                       z, B, S, g_ro, g_rd);
+    NR_LAUNCH_CHECK("nr_pts_bwd");
+    return NR_OK;
+}
+
+int nr_viewdirs_bwd(const float* rd, const float* g_vd, int B, int S, float* g_rd, nr_stream_t stream) {
+    NR_REQUIRE(rd && g_vd && g_rd && B >= 0 && S > 0, "nr_viewdirs_bwd: bad arguments");
+    if (B == 0) return NR_OK;
+    hipLaunchKernelGGL(viewdirs_bwd_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       rd, g_vd, B, S, g_rd);
+    NR_LAUNCH_CHECK("nr_viewdirs_bwd");
+    return NR_OK;
+}
+
+}  // extern "C"

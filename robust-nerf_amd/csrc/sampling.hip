@@ -1,0 +1,182 @@
+// Inverse-CDF (hierarchical) sampling, one wave per ray.
+//
+// Reference semantics (ShawnnnLiu/Robust-NeRF):
+//   sample_pdf           noisy_src/rays.py:213-279
+//   sample_hierarchical  noisy_src/rays.py:282-333
+// Per ray: w += 1e-5; pdf = w / sum(w); cdf = [0, cumsum(pdf)] (sequential
+// order, as torch's CPU cumsum); u = linspace(0,1,Ns) if det else the caller's
+// uniforms; idx = searchsorted(cdf, u, right=True); below/above clamped; the
+// `denom < 1e-5 -> 1` rule; s = b0 + (u-c0)/denom * (b1-b0).  The hierarchical
+// form then sorts cat(z_coarse, s) — here an all-pairs rank sort in LDS, whose
+// output values equal torch.sort's whatever the order of u.
+#include "common.hpp"
+
+namespace nr {
+
+constexpr int kRaysPerBlock = 4;  // one wave per ray
+constexpr int kMaxPerLane = 8;    // Nc + Nf <= 512
+
+__device__ __forceinline__ float linspace01(int n, int i) {
+    if (n == 1) return 0.f;
+    const float step = 1.0f / static_cast<float>(n - 1);
+    return i < n / 2 ? step * static_cast<float>(i) : 1.0f - step * static_cast<float>(n - 1 - i);
+}
+
+// Build cdf[0..nb-1] from wbuf[0..nb-2] (raw weights, +1e-5 applied here).
+// Every lane runs the same sequential recurrence; the owner lane stores.
+__device__ __forceinline__ void build_cdf(const float* wbuf, float* cdf, int nb, int lane) {
+    const int nw = nb - 1;
+    float sum = 0.f;
+    for (int k = 0; k < nw; ++k) sum += wbuf[k] + 1e-5f;
+    float run = 0.f;
+    if (lane == 0) cdf[0] = 0.f;
+    for (int k = 0; k < nw; ++k) {
+        run += (wbuf[k] + 1e-5f) / sum;
+        if (((k + 1) & 63) == lane) cdf[k + 1] = run;
+    }
+}
+
+__device__ __forceinline__ float invert_cdf(const float* cdf, const float* bins, int nb, float u) {
+    int lo = 0, hi = nb;  // first index with cdf[idx] > u  (searchsorted right=True)
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cdf[mid] > u)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    const int below = lo - 1 > 0 ? lo - 1 : 0;
+    const int above = lo < nb - 1 ? lo : nb - 1;
+    const float c0 = cdf[below], c1 = cdf[above];
+    const float b0 = bins[below], b1 = bins[above];
+    float denom = c1 - c0;
+    denom = denom < 1e-5f ? 1.0f : denom;
+    const float t = (u - c0) / denom;
+    return b0 + t * (b1 - b0);
+}
+
+// LDS per wave: bins[nb] | cdf[nb] | wbuf[nb] | uni[T]
+__global__ void sample_pdf_kernel(const float* bins_g, const float* w_g, const float* u_g, int B, int Nb, int Ns,
+                                  float* out) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int b = blockIdx.x * kRaysPerBlock + wv;
+    float* bins = smem + wv * (3 * Nb);
+    float* cdf = bins + Nb;
+    float* wbuf = cdf + Nb;
+    const bool live = b < B;
+    if (live) {
+        for (int i = lane; i < Nb; i += 64) bins[i] = bins_g[static_cast<int64_t>(b) * Nb + i];
+        for (int i = lane; i < Nb - 1; i += 64) wbuf[i] = w_g[static_cast<int64_t>(b) * (Nb - 1) + i];
+    }
+    __syncthreads();
+    if (live) build_cdf(wbuf, cdf, Nb, lane);
+    __syncthreads();
+    if (!live) return;
+    for (int j = lane; j < Ns; j += 64) {
+        const float u = u_g ? u_g[static_cast<int64_t>(b) * Ns + j] : linspace01(Ns, j);
+        out[static_cast<int64_t>(b) * Ns + j] = invert_cdf(cdf, bins, Nb, u);
+    }
+}
+
+__global__ void sample_hier_kernel(const float* ro, const float* rd, const float* zc_g, const float* wc_g,
+                                   const float* u_g, int B, int Nc, int Nf, float* zf_out, float* pts_out) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int b = blockIdx.x * kRaysPerBlock + wv;
+    const int Nb = Nc - 1, T = Nc + Nf;
+    float* bins = smem + wv * (3 * Nb + T);
+    float* cdf = bins + Nb;
+    float* wbuf = cdf + Nb;
+    float* uni = wbuf + Nb;
+    const bool live = b < B;
+    const int64_t zb = static_cast<int64_t>(b) * Nc;
+    if (live) {
+        for (int i = lane; i < Nc; i += 64) uni[i] = zc_g[zb + i];
+        for (int i = lane; i < Nc - 2; i += 64) wbuf[i] = wc_g[zb + 1 + i];  // weights[..., 1:-1]
+    }
+    __syncthreads();
+    if (live) {
+        for (int i = lane; i < Nb; i += 64) bins[i] = 0.5f * (uni[i + 1] + uni[i]);  // z_vals_mid
+        build_cdf(wbuf, cdf, Nb, lane);
+    }
+    __syncthreads();
+    if (live) {
+        for (int j = lane; j < Nf; j += 64) {
+            const float u = u_g ? u_g[static_cast<int64_t>(b) * Nf + j] : linspace01(Nf, j);
+            uni[Nc + j] = invert_cdf(cdf, bins, Nb, u);
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    // all-pairs rank sort of uni[0..T): rank = #{q: x_q < x} + #{q < e: x_q == x}
+    float v[kMaxPerLane];
+    int rank[kMaxPerLane];
+#pragma unroll
+    for (int k = 0; k < kMaxPerLane; ++k) {
+        const int e = lane + 64 * k;
+        v[k] = e < T ? uni[e] : 0.f;
+        rank[k] = 0;
+    }
+    for (int q = 0; q < T; ++q) {
+        const float x = uni[q];
+#pragma unroll
+        for (int k = 0; k < kMaxPerLane; ++k) {
+            const int e = lane + 64 * k;
+            rank[k] += (x < v[k]) || (x == v[k] && q < e);
+        }
+    }
+    const int64_t ob = static_cast<int64_t>(b) * T;
+    float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 0.f, dz = 0.f;
+    if (pts_out) {
+        ox = ro[3 * b], oy = ro[3 * b + 1], oz = ro[3 * b + 2];
+        dx = rd[3 * b], dy = rd[3 * b + 1], dz = rd[3 * b + 2];
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxPerLane; ++k) {
+        const int e = lane + 64 * k;
+        if (e < T) {
+            const int64_t o = ob + rank[k];
+            zf_out[o] = v[k];
+            if (pts_out) {
+                pts_out[3 * o] = ox + dx * v[k];
+                pts_out[3 * o + 1] = oy + dy * v[k];
+                pts_out[3 * o + 2] = oz + dz * v[k];
+            }
+        }
+    }
+}
+
+}  // namespace nr
+
+using namespace nr;
+
+extern "C" {
+
+int nr_sample_pdf(const float* bins, const float* weights, const float* u, int B, int Nb, int Ns, float* samples,
+                  nr_stream_t stream) {
+    NR_REQUIRE(bins && weights && samples && B >= 0 && Nb >= 2 && Ns > 0, "nr_sample_pdf: bad arguments");
+    if (B == 0) return NR_OK;
+    const size_t lds = sizeof(float) * kRaysPerBlock * 3 * Nb;
+    NR_REQUIRE(lds <= 64 * 1024, "nr_sample_pdf: Nb=%d too large", Nb);
+    hipLaunchKernelGGL(sample_pdf_kernel, dim3(ceil_div(B, kRaysPerBlock)), dim3(64 * kRaysPerBlock), lds,
+                       static_cast<hipStream_t>(stream), bins, weights, u, B, Nb, Ns, samples);
+    NR_LAUNCH_CHECK("nr_sample_pdf");
+    return NR_OK;
+}
+
+int nr_sample_hierarchical(const float* ro, const float* rd, const float* zc, const float* wc, const float* u,
+                           int B, int Nc, int Nf, float* zf, float* pts, nr_stream_t stream) {
+    NR_REQUIRE(zc && wc && zf && B >= 0 && Nc >= 3 && Nf > 0 && (!pts || (ro && rd)),
+               "nr_sample_hierarchical: bad arguments");
+    NR_REQUIRE(Nc + Nf <= 64 * kMaxPerLane, "nr_sample_hierarchical: Nc+Nf=%d exceeds %d", Nc + Nf,
+               64 * kMaxPerLane);
+    if (B == 0) return NR_OK;
+    const size_t lds = sizeof(float) * kRaysPerBlock * (3 * (Nc - 1) + Nc + Nf);
+    hipLaunchKernelGGL(sample_hier_kernel, dim3(ceil_div(B, kRaysPerBlock)), dim3(64 * kRaysPerBlock), lds,
+                       static_cast<hipStream_t>(stream), ro, rd, zc, wc, u, B, Nc, Nf, zf, pts);
+    NR_LAUNCH_CHECK("nr_sample_hierarchical");
+    return NR_OK;
+}
+
+}  // extern "C"

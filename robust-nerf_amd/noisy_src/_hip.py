@@ -24,6 +24,7 @@ c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
 c_i64 = ctypes.c_int64
 c_f = ctypes.c_float
+c_d = ctypes.c_double
 c_u32 = ctypes.c_uint32
 
 
@@ -74,7 +75,7 @@ _SIGNATURES = {
     "nr_mlp_backward": (c_i, [_cfg_p, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_vp, c_vp, c_vp, c_vp, c_vp]),
     "nr_sumsq": (c_i, [c_vp, c_i64, c_vp, c_vp]),
-    "nr_adam_step": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_f, c_f, c_f, c_f, c_i64, c_vp, c_f, c_vp]),
+    "nr_adam_step": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_d, c_d, c_d, c_d, c_i64, c_vp, c_f, c_vp]),
     "nr_expand_viewdirs": (c_i, [c_vp, c_i, c_i, c_vp, c_vp]),
     "nr_pts_bwd": (c_i, [c_vp, c_vp, c_i, c_i, c_vp, c_vp, c_vp]),
     "nr_viewdirs_bwd": (c_i, [c_vp, c_vp, c_i, c_i, c_vp, c_vp]),

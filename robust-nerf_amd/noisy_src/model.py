@@ -1,0 +1,221 @@
+"""
+NeRF model — drop-in for ShawnnnLiu/Robust-NeRF ``noisy_src/model.py:20-221``.
+
+``NeRF`` registers exactly the reference's submodules (``pts_linears.{i}``,
+``sigma_linear``, ``feature_linear``, ``dir_linear``, ``rgb_linear``,
+``pos_encoder.freq_bands``, ``dir_encoder.freq_bands``), built in the same order
+with the same ``nn.Linear`` default init, so ``torch.manual_seed(s)`` gives the
+reference's initial weights and checkpoints are interchangeable.
+
+Underneath, the parameters are views into one flat fp32 buffer (the C-ABI
+layout) and ``forward`` is a single fused HIP kernel (positional encoding, 8
+trunk layers, skip concat, sigma/feature/dir/rgb heads) whose backward is the
+fused dX chain + dW GEMM (csrc/mlp.hip).  ``ModelConfig.precision`` selects the
+fp32 (parity) or bf16 MFMA path.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _hip, ops
+from ._hip import NrMlpConfig, call, ptr
+from .config import ModelConfig
+
+
+class PositionalEncoding(nn.Module):
+    """Reference model.py:20-80: [x, sin(f0 x), cos(f0 x), ...], f = 2^k, no pi."""
+
+    def __init__(self, num_freqs: int, include_input: bool = True, log_sampling: bool = True) -> None:
+        super().__init__()
+        self.num_freqs = num_freqs
+        self.include_input = include_input
+        self.log_sampling = log_sampling
+        if log_sampling:
+            freq_bands = 2.0 ** torch.linspace(0.0, num_freqs - 1, num_freqs)
+        else:
+            freq_bands = torch.linspace(1.0, 2.0 ** (num_freqs - 1), num_freqs)
+        self.register_buffer("freq_bands", freq_bands)
+
+    @property
+    def output_dim(self) -> int:
+        dim = 2 * self.num_freqs
+        if self.include_input:
+            dim += 1
+        return dim
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return ops.positional_encoding(x, self.num_freqs, self.include_input, self.log_sampling)
+
+
+def _precision_code(p: str) -> int:
+    if p == "fp32":
+        return _hip.NR_PREC_FP32
+    if p == "bf16":
+        return _hip.NR_PREC_BF16
+    raise ValueError(f"ModelConfig.precision must be 'fp32' or 'bf16', got {p!r}")
+
+
+class _MLPFunction(torch.autograd.Function):
+    """Fused NeRF MLP forward/backward on MFMA (csrc/mlp.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, d, net, *params):
+        cfg = ctypes.byref(net._nr_cfg)
+        flat = net._flat
+        packed = net._packed_for_forward()
+        xc = ops._c(x)
+        dc = ops._c(d) if d is not None else None
+        M = xc.shape[0]
+        rgb = torch.empty(M, 3, device=xc.device, dtype=torch.float32)
+        sigma = torch.empty(M, 1, device=xc.device, dtype=torch.float32)
+        training = any(ctx.needs_input_grad)
+        saved = None
+        if training and M > 0:
+            saved = torch.empty(int(_hip.load().nr_mlp_saved_bytes(cfg, M)), device=xc.device, dtype=torch.uint8)
+        call("nr_mlp_forward", cfg, ptr(packed), ptr(flat), ptr(xc), ptr(dc), M, ptr(rgb), ptr(sigma), ptr(saved),
+             _hip.stream_ptr())
+        if training:
+            ctx.save_for_backward(xc, dc if dc is not None else xc.new_empty(0), rgb, sigma)
+            ctx.has_d = dc is not None
+            ctx.keep = (net, saved, packed, flat)
+        return rgb, sigma
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_sigma):
+        xc, dc, rgb, sigma = ctx.saved_tensors
+        net, saved, packed, flat = ctx.keep
+        cfg = ctypes.byref(net._nr_cfg)
+        M = xc.shape[0]
+        dev = xc.device
+        g_rgb = ops._c(g_rgb) if g_rgb is not None else torch.zeros(M, 3, device=dev)
+        g_sigma = ops._c(g_sigma) if g_sigma is not None else torch.zeros(M, 1, device=dev)
+        gflat = torch.empty(net._param_count, device=dev, dtype=torch.float32)
+        g_x = torch.empty(M, 3, device=dev) if ctx.needs_input_grad[0] else None
+        g_d = torch.empty(M, 3, device=dev) if (ctx.needs_input_grad[1] and ctx.has_d) else None
+        if M > 0:
+            ws = torch.empty(int(_hip.load().nr_mlp_workspace_bytes(cfg, M)), device=dev, dtype=torch.uint8)
+            call("nr_mlp_backward", cfg, ptr(packed), ptr(flat), ptr(xc), ptr(dc) if ctx.has_d else None, M, ptr(rgb),
+                 ptr(sigma), ptr(saved), ptr(g_rgb), ptr(g_sigma), ptr(gflat), ptr(g_x), ptr(g_d), ptr(ws),
+                 _hip.stream_ptr())
+        else:
+            gflat.zero_()
+        grads = []
+        off = 0
+        for p in net._param_list:
+            n = p.numel()
+            grads.append(gflat[off:off + n].view(p.shape))
+            off += n
+        return (g_x, g_d, None, *grads)
+
+
+class NeRF(nn.Module):
+    """Reference model.py:83-196 (same submodules, parameter order and init)."""
+
+    def __init__(self, config: ModelConfig | None = None) -> None:
+        super().__init__()
+        if config is None:
+            config = ModelConfig()
+        self.config = config
+        self.pos_encoder = PositionalEncoding(num_freqs=config.pos_freqs, include_input=True)
+        self.dir_encoder = PositionalEncoding(num_freqs=config.dir_freqs, include_input=True)
+        pos_dim = 3 * self.pos_encoder.output_dim
+        dir_dim = 3 * self.dir_encoder.output_dim
+        self.pts_linears = nn.ModuleList()
+        in_dim = pos_dim
+        for i in range(config.num_hidden_layers):
+            self.pts_linears.append(nn.Linear(in_dim, config.hidden_dim))
+            in_dim = config.hidden_dim
+            if i in config.skips:
+                in_dim += pos_dim
+        self.sigma_linear = nn.Linear(config.hidden_dim, 1)
+        self.feature_linear = nn.Linear(config.hidden_dim, config.hidden_dim)
+        if config.use_view_dirs:
+            self.dir_linear = nn.Linear(config.hidden_dim + dir_dim, config.hidden_dim // 2)
+        else:
+            self.dir_linear = nn.Linear(config.hidden_dim, config.hidden_dim // 2)
+        self.rgb_linear = nn.Linear(config.hidden_dim // 2, 3)
+
+        skip_mask = 0
+        for s in config.skips:
+            skip_mask |= 1 << int(s)
+        self._nr_cfg = NrMlpConfig(
+            pos_freqs=config.pos_freqs, dir_freqs=config.dir_freqs, hidden=config.hidden_dim,
+            n_layers=config.num_hidden_layers, skip_mask=skip_mask, use_view_dirs=int(bool(config.use_view_dirs)),
+            precision=_precision_code(getattr(config, "precision", "fp32")))
+        self._param_count = sum(p.numel() for p in self.parameters())
+        self._flat: Optional[torch.Tensor] = None
+        self._packed: Optional[torch.Tensor] = None
+        self._packed_key = None
+
+    # -- flat parameter buffer -------------------------------------------------
+    @property
+    def _param_list(self) -> List[nn.Parameter]:
+        return list(self.parameters())
+
+    def flat_params(self) -> torch.Tensor:
+        """The flat fp32 buffer every parameter is a view of (C-ABI layout)."""
+        self._ensure_flat()
+        return self._flat
+
+    def _ensure_flat(self) -> None:
+        params = self._param_list
+        flat = self._flat
+        if flat is not None and flat.device == params[0].device:
+            off = 0
+            base = flat.data_ptr()
+            ok = True
+            for p in params:
+                if p.data_ptr() != base + 4 * off or not p.is_contiguous():
+                    ok = False
+                    break
+                off += p.numel()
+            if ok:
+                return
+        dev = params[0].device
+        _hip.require_device(params[0])
+        flat = torch.empty(self._param_count, device=dev, dtype=torch.float32)
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                n = p.numel()
+                flat[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = flat[off:off + n].view(p.shape)
+                off += n
+        self._flat = flat
+        self._packed_key = None
+
+    def _packed_for_forward(self) -> torch.Tensor:
+        params = self._param_list
+        key = (self._flat.data_ptr(), tuple(p._version for p in params))
+        if self._packed is None or self._packed_key != key or self._packed.device != self._flat.device:
+            cfg = ctypes.byref(self._nr_cfg)
+            nbytes = int(_hip.load().nr_mlp_packed_bytes(cfg))
+            if nbytes < 0:
+                raise RuntimeError(f"NeRF config unsupported by the HIP MLP: {_hip.last_error()}")
+            self._packed = torch.empty(nbytes, device=self._flat.device, dtype=torch.uint8)
+            call("nr_mlp_pack", cfg, ptr(self._flat), ptr(self._packed), _hip.stream_ptr())
+            self._packed_key = key
+        return self._packed
+
+    def forward(self, x: torch.Tensor, d: torch.Tensor | None = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """x (N,3) positions, d (N,3) view dirs -> rgb (N,3) in [0,1], sigma (N,1) >= 0."""
+        _hip.require_device(x, d)
+        if self.config.use_view_dirs and d is None:
+            # reference model.py:187-193 would feed 256 features to a 283-input layer
+            raise ValueError("NeRF with use_view_dirs=True needs view directions d")
+        self._ensure_flat()
+        return _MLPFunction.apply(x, d if self.config.use_view_dirs else None, self, *self._param_list)
+
+
+def create_nerf(config: ModelConfig | None = None) -> Tuple[NeRF, NeRF | None]:
+    """Reference model.py:199-221: coarse and fine networks of the same architecture."""
+    if config is None:
+        config = ModelConfig()
+    model_coarse = NeRF(config)
+    model_fine = NeRF(config)
+    return model_coarse, model_fine

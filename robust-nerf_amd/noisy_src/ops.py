@@ -1,0 +1,339 @@
+"""Host-side operators over the C ABI (include/nerf_hip.h), with autograd.
+
+Each function allocates its outputs with the PyTorch caching allocator, hands
+raw device pointers to one ``nr_*`` entry point on the current HIP stream and,
+where the reference path is differentiable, is wrapped in a
+``torch.autograd.Function`` whose backward is the matching HIP kernel.  There
+is no CPU or eager-torch fallback: CPU tensors raise.
+"""
+
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _hip
+from ._hip import call, ptr
+
+_f32 = torch.float32
+
+
+def _stream() -> int:
+    return _hip.stream_ptr()
+
+
+def _c(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """Contiguous fp32 view (no copy when already so)."""
+    if t is None:
+        return None
+    if t.dtype != _f32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _check(*ts):
+    _hip.require_device(*ts)
+
+
+# ---------------------------------------------------------------- A1 / A2 ----
+def ray_directions(H: int, W: int, focal: float, cx: float, cy: float, device) -> torch.Tensor:
+    out = torch.empty(H, W, 3, device=device, dtype=_f32)
+    if not out.is_cuda:
+        _check(out)
+    call("nr_ray_directions", H, W, float(focal), float(cx), float(cy), ptr(out), _stream())
+    return out
+
+
+def get_rays(directions: torch.Tensor, c2w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    _check(directions, c2w)
+    d = _c(directions)
+    c = _c(c2w)
+    shape = d.shape
+    n = d.numel() // 3
+    ro = torch.empty(shape, device=d.device, dtype=_f32)
+    rd = torch.empty(shape, device=d.device, dtype=_f32)
+    call("nr_get_rays", ptr(d), ptr(c), n, ptr(ro), ptr(rd), _stream())
+    return ro, rd
+
+
+# ---------------------------------------------------------------- A5 / A9 / A10
+def _pts_bwd(ctx, g_pts, z):
+    """pts = o + d * z (rays.py:208 / :331): sum the sample gradients per ray."""
+    g_o = g_d = None
+    if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+        B, S = z.shape
+        g_o = torch.zeros(B, 3, device=z.device, dtype=_f32) if ctx.needs_input_grad[0] else None
+        g_d = torch.zeros(B, 3, device=z.device, dtype=_f32) if ctx.needs_input_grad[1] else None
+        call("nr_pts_bwd", ptr(_c(g_pts)), ptr(z), B, S, ptr(g_o), ptr(g_d), _stream())
+    return g_o, g_d
+
+
+class _Stratified(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, rays_o, rays_d, t_rand, near, far, lindisp, num_samples):
+        ro, rd = _c(rays_o), _c(rays_d)
+        B = ro.shape[0]
+        z = torch.empty(B, num_samples, device=ro.device, dtype=_f32)
+        pts = torch.empty(B, num_samples, 3, device=ro.device, dtype=_f32)
+        tr = _c(t_rand)
+        call("nr_stratified_sample", ptr(ro), ptr(rd), ptr(tr), float(near), float(far), int(bool(lindisp)), B,
+             num_samples, ptr(z), ptr(pts), _stream())
+        ctx.save_for_backward(z)
+        ctx.mark_non_differentiable(z)
+        return pts, z
+
+    @staticmethod
+    def backward(ctx, g_pts, _g_z):
+        (z,) = ctx.saved_tensors
+        g_o, g_d = _pts_bwd(ctx, g_pts, z)
+        return g_o, g_d, None, None, None, None, None
+
+
+def stratified_sample(rays_o, rays_d, near, far, num_samples, t_rand=None, lindisp=False):
+    """Returns (pts (B,N,3), z (B,N)); t_rand None -> no perturbation."""
+    _check(rays_o, rays_d, t_rand)
+    return _Stratified.apply(rays_o, rays_d, t_rand, near, far, lindisp, num_samples)
+
+
+def sample_pdf(bins, weights, num_samples, u=None):
+    _check(bins, weights, u)
+    b, w = _c(bins.detach()), _c(weights.detach())
+    lead = b.shape[:-1]
+    Nb = b.shape[-1]
+    B = b.numel() // Nb
+    uu = _c(u.detach()) if u is not None else None
+    out = torch.empty(*lead, num_samples, device=b.device, dtype=_f32)
+    call("nr_sample_pdf", ptr(b), ptr(w), ptr(uu), B, Nb, num_samples, ptr(out), _stream())
+    return out
+
+
+class _Hierarchical(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, rays_o, rays_d, z_coarse, w_coarse, u, num_samples_fine):
+        ro, rd = _c(rays_o), _c(rays_d)
+        zc, wc = _c(z_coarse), _c(w_coarse)
+        B, Nc = zc.shape
+        T = Nc + num_samples_fine
+        zf = torch.empty(B, T, device=zc.device, dtype=_f32)
+        pts = torch.empty(B, T, 3, device=zc.device, dtype=_f32)
+        uu = _c(u)
+        call("nr_sample_hierarchical", ptr(ro), ptr(rd), ptr(zc), ptr(wc), ptr(uu), B, Nc, num_samples_fine,
+             ptr(zf), ptr(pts), _stream())
+        ctx.save_for_backward(zf)
+        ctx.mark_non_differentiable(zf)
+        return pts, zf
+
+    @staticmethod
+    def backward(ctx, g_pts, _g_z):
+        (zf,) = ctx.saved_tensors
+        g_o, g_d = _pts_bwd(ctx, g_pts, zf)
+        return g_o, g_d, None, None, None, None
+
+
+def sample_hierarchical(rays_o, rays_d, z_coarse, w_coarse, num_samples_fine, u=None):
+    """Returns (pts_fine (B,Nc+Nf,3), z_fine (B,Nc+Nf)); u None -> det.  The fine
+    depths are detached as in the reference (rays.py:325)."""
+    _check(rays_o, rays_d, z_coarse, w_coarse, u)
+    return _Hierarchical.apply(rays_o, rays_d, z_coarse.detach(), w_coarse.detach(),
+                               u.detach() if u is not None else None, num_samples_fine)
+
+
+# ---------------------------------------------------------------- viewdirs ---
+class _ExpandViewdirs(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, rays_d, S):
+        rd = _c(rays_d)
+        B = rd.shape[0]
+        out = torch.empty(B * S, 3, device=rd.device, dtype=_f32)
+        call("nr_expand_viewdirs", ptr(rd), B, S, ptr(out), _stream())
+        ctx.save_for_backward(rd)
+        ctx.S = S
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (rd,) = ctx.saved_tensors
+        g_rd = torch.zeros_like(rd)
+        call("nr_viewdirs_bwd", ptr(rd), ptr(_c(g)), rd.shape[0], ctx.S, ptr(g_rd), _stream())
+        return g_rd, None
+
+
+def expand_viewdirs(rays_d: torch.Tensor, S: int) -> torch.Tensor:
+    """normalize(rays_d) repeated for S samples per ray -> (B*S, 3) (rendering.py:165,182)."""
+    _check(rays_d)
+    return _ExpandViewdirs.apply(rays_d, S)
+
+
+# ---------------------------------------------------------------- A6 ---------
+class _PosEnc(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, L, include_input, log_sampling):
+        xc = _c(x)
+        C = xc.shape[-1]
+        M = xc.numel() // C
+        D = (1 if include_input else 0) + 2 * L
+        out = torch.empty(*xc.shape[:-1], C * D, device=xc.device, dtype=_f32)
+        call("nr_positional_encoding", ptr(xc), M, C, L, int(include_input), int(log_sampling), ptr(out), _stream())
+        ctx.save_for_backward(xc)
+        ctx.args = (L, include_input, log_sampling)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (xc,) = ctx.saved_tensors
+        L, inc, logs = ctx.args
+        C = xc.shape[-1]
+        gx = torch.empty_like(xc)
+        call("nr_positional_encoding_bwd", ptr(xc), xc.numel() // C, C, L, int(inc), int(logs), ptr(_c(g)), ptr(gx),
+             _stream())
+        return gx, None, None, None
+
+
+def positional_encoding(x, num_freqs, include_input=True, log_sampling=True):
+    _check(x)
+    return _PosEnc.apply(x, num_freqs, include_input, log_sampling)
+
+
+# ---------------------------------------------------------------- A8 ---------
+class _Composite(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, rgb, sigma, z, rays_d, noise, white):
+        rgb, sigma, z, rd = _c(rgb), _c(sigma), _c(z), _c(rays_d)
+        B, S = z.shape
+        nz = _c(noise)
+        rgb_map = torch.empty(B, 3, device=z.device, dtype=_f32)
+        depth = torch.empty(B, device=z.device, dtype=_f32)
+        acc = torch.empty(B, device=z.device, dtype=_f32)
+        weights = torch.empty(B, S, device=z.device, dtype=_f32)
+        call("nr_composite_fwd", ptr(rgb), ptr(sigma), ptr(z), ptr(rd), ptr(nz), B, S, int(white), ptr(rgb_map),
+             ptr(depth), ptr(acc), ptr(weights), _stream())
+        ctx.save_for_backward(rgb, sigma, z, rd, nz)
+        ctx.white = white
+        return rgb_map, depth, acc, weights
+
+    @staticmethod
+    def backward(ctx, g_map, g_depth, g_acc, g_w):
+        rgb, sigma, z, rd, nz = ctx.saved_tensors
+        B, S = z.shape
+        if g_map is None:
+            g_map = torch.zeros(B, 3, device=z.device, dtype=_f32)
+        g_rgb = torch.empty_like(rgb)
+        g_sigma = torch.empty(B, S, device=z.device, dtype=_f32)
+        g_rd = torch.zeros_like(rd) if ctx.needs_input_grad[3] else None
+        call("nr_composite_bwd", ptr(rgb), ptr(sigma), ptr(z), ptr(rd), ptr(nz), B, S, int(ctx.white),
+             ptr(_c(g_map)), ptr(_c(g_depth)), ptr(_c(g_acc)), ptr(_c(g_w)), ptr(g_rgb), ptr(g_sigma), ptr(g_rd),
+             _stream())
+        return g_rgb, g_sigma.view(sigma.shape), None, g_rd, None, None
+
+
+def composite(rgb, sigma, z_vals, rays_d, noise=None, white_background=True):
+    """raw2outputs core: rgb (B,S,3), sigma (B,S[,1]), z (B,S), rays_d (B,3)."""
+    _check(rgb, sigma, z_vals, rays_d, noise)
+    sig = sigma.reshape(z_vals.shape)
+    return _Composite.apply(rgb, sig, z_vals, rays_d, noise, bool(white_background))
+
+
+# ---------------------------------------------------------------- A3 / A4 ----
+class _RaysFromPixels(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img_idx, pix, poses, H, W, focal):
+        img = img_idx.to(torch.int64).contiguous()
+        px, ps = _c(pix), _c(poses)
+        B = img.shape[0]
+        ro = torch.empty(B, 3, device=px.device, dtype=_f32)
+        rd = torch.empty(B, 3, device=px.device, dtype=_f32)
+        call("nr_rays_from_pixels_fwd", ptr(img), ptr(px), ptr(ps), ps.shape[0], H, W, float(focal), B, ptr(ro),
+             ptr(rd), _stream())
+        ctx.save_for_backward(img, px, ps)
+        ctx.args = (H, W, float(focal))
+        return ro, rd
+
+    @staticmethod
+    def backward(ctx, g_ro, g_rd):
+        img, px, ps = ctx.saved_tensors
+        H, W, focal = ctx.args
+        B = img.shape[0]
+        if g_ro is None:
+            g_ro = torch.zeros(B, 3, device=px.device, dtype=_f32)
+        g_poses = torch.zeros_like(ps)
+        call("nr_rays_from_pixels_bwd", ptr(img), ptr(px), ptr(ps), ps.shape[0], H, W, focal, B, ptr(_c(g_ro)),
+             ptr(_c(g_rd)), ptr(g_poses), _stream())
+        return None, None, g_poses, None, None, None
+
+
+def rays_from_pixels(img_idx, pix, poses, H, W, focal):
+    """get_rays_from_pixels (data_pose_opt.py:83-148) in one pass; poses indexed by img_idx."""
+    _check(img_idx, pix, poses)
+    return _RaysFromPixels.apply(img_idx, pix, poses, H, W, focal)
+
+
+class _Se3Poses(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, init, rot, trans, indices, fixed_small_angle):
+        ini = _c(init)
+        r = _c(rot.detach()) if rot is not None else None
+        t = _c(trans.detach()) if trans is not None else None
+        idx = indices.to(torch.int64).contiguous() if indices is not None else None
+        n = idx.shape[0] if idx is not None else ini.shape[0]
+        out = torch.empty(n, 4, 4, device=ini.device, dtype=_f32)
+        call("nr_se3_poses_fwd", ptr(ini), ptr(r), ptr(t), ptr(idx), n, ptr(out), _stream())
+        ctx.save_for_backward(ini, r if r is not None else ini.new_empty(0), idx if idx is not None else ini.new_empty(0, dtype=torch.int64))
+        ctx.flags = (r is not None, t is not None, idx is not None, n, bool(fixed_small_angle))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        ini, r, idx = ctx.saved_tensors
+        has_r, has_t, has_idx, n, fixed = ctx.flags
+        g_rot = torch.zeros(ini.shape[0], 3, device=ini.device, dtype=_f32) if (has_r and ctx.needs_input_grad[1]) else None
+        g_trans = torch.zeros(ini.shape[0], 3, device=ini.device, dtype=_f32) if (has_t and ctx.needs_input_grad[2]) else None
+        call("nr_se3_poses_bwd", ptr(ini), ptr(r) if has_r else None, ptr(idx) if has_idx else None, n, ptr(_c(g)),
+             int(fixed), ptr(g_rot), ptr(g_trans), _stream())
+        return None, g_rot, g_trans, None, None
+
+
+def se3_poses(init_poses, rot_deltas=None, trans_deltas=None, indices=None, fixed_small_angle=False):
+    _check(init_poses, rot_deltas, trans_deltas, indices)
+    return _Se3Poses.apply(init_poses, rot_deltas, trans_deltas, indices, fixed_small_angle)
+
+
+# ---------------------------------------------------------------- loss -------
+def mse_loss_and_grad(pred, target, scale=1.0):
+    """(loss (device scalar), d loss/d pred * scale) for mean((pred-target)^2)."""
+    _check(pred, target)
+    p, t = _c(pred), _c(target)
+    loss = torch.empty((), device=p.device, dtype=_f32)
+    g = torch.empty_like(p)
+    call("nr_mse_fwd_bwd", ptr(p), ptr(t), p.shape[0], float(scale), ptr(loss), ptr(g), _stream())
+    return loss, g
+
+
+# ---------------------------------------------------------------- optimizer --
+def sumsq_into(x: torch.Tensor, acc: torch.Tensor) -> None:
+    call("nr_sumsq", ptr(x), x.numel(), ptr(acc), _stream())
+
+
+def adam_step(p, g, m, v, lr, beta1, beta2, eps, step, sumsq=None, max_norm=1.0):
+    call("nr_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr), float(beta1), float(beta2), float(eps),
+         int(step), ptr(sumsq), float(max_norm), _stream())
+
+
+class _MSE(torch.autograd.Function):
+    """mean((pred - target)^2) (train.py:89); the gradient is produced in the same kernel."""
+
+    @staticmethod
+    def forward(ctx, pred, target):
+        loss, g = mse_loss_and_grad(pred, target)
+        ctx.save_for_backward(g)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        (g,) = ctx.saved_tensors
+        return g * gl, None
+
+
+def mse_loss(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    _check(pred, target)
+    return _MSE.apply(pred, target)

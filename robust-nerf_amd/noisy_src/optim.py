@@ -1,0 +1,161 @@
+"""
+Optimizer tail on HIP: Adam + global-norm gradient clipping.
+
+Replaces the reference's ``torch.optim.Adam`` + ``clip_grad_norm_`` sequence
+(noisy_src/train.py:112-117, noisy_src/train_pose_opt.py:398-409) with the
+fused kernel ``nr_adam_step`` (csrc/optim.hip): one launch per run of
+parameters that are contiguous in one flat buffer (a NeRF network is one run),
+with the clip coefficient computed on the device from ``nr_sumsq`` — no host
+synchronisation.  ``FusedAdam`` is a ``torch.optim.Optimizer``, so
+``LambdaLR``/``state_dict`` work as with torch's Adam.
+"""
+
+from __future__ import annotations
+
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import ops
+
+
+def _contiguous_run(ts: Sequence[torch.Tensor]) -> Optional[torch.Tensor]:
+    """A 1-D view covering ``ts`` if they lie back to back in one storage, else None."""
+    if not ts:
+        return None
+    base = ts[0]
+    st = base.untyped_storage()
+    off = base.storage_offset()
+    n = 0
+    for t in ts:
+        if (t.untyped_storage().data_ptr() != st.data_ptr() or t.storage_offset() != off + n
+                or not t.is_contiguous() or t.dtype != torch.float32):
+            return None
+        n += t.numel()
+    return torch.empty(0, dtype=torch.float32, device=base.device).set_(st, off, (n,), (1,))
+
+
+def _runs(params: List[torch.Tensor]) -> List[List[torch.Tensor]]:
+    """Split params into maximal runs that are contiguous in memory."""
+    runs, cur = [], []
+    for p in params:
+        if cur and _contiguous_run(cur + [p]) is None:
+            runs.append(cur)
+            cur = []
+        cur.append(p)
+    if cur:
+        runs.append(cur)
+    return runs
+
+
+def grad_sumsq(params: Iterable[torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Device scalar sum of squares of all gradients (HIP reduction, no host sync)."""
+    params = [p for p in params if p.grad is not None]
+    if out is None:
+        out = torch.zeros((), device=params[0].device, dtype=torch.float32)
+    for run in _runs([p.grad for p in params]):
+        flat = _contiguous_run(run)
+        if flat is None or flat.data_ptr() % 16:
+            flat = torch.cat([g.reshape(-1) for g in run])
+        ops.sumsq_into(flat, out)
+    return out
+
+
+def clip_grad_norm_(parameters, max_norm: float) -> torch.Tensor:
+    """torch.nn.utils.clip_grad_norm_ semantics (coef = min(1, max_norm/(norm+1e-6)))."""
+    if isinstance(parameters, torch.Tensor):
+        parameters = [parameters]
+    params = [p for p in parameters if p.grad is not None]
+    if not params:
+        return torch.zeros(())
+    total = grad_sumsq(params).sqrt()
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    for p in params:
+        p.grad.mul_(coef)
+    return total
+
+
+class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam (amsgrad=False, weight_decay=0) on the HIP fused kernel.
+
+    ``step(clip_groups=[(params, max_norm), ...])`` folds clip_grad_norm_ of each
+    group into the update (train.py:115 joint clip; train_pose_opt.py:398-404
+    per-network clips)."""
+
+    def __init__(self, params, lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999), eps: float = 1e-8):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+        self._flat_state = {}
+
+    def _state_run(self, run: List[torch.nn.Parameter]):
+        key = tuple(id(p) for p in run)
+        cached = self._flat_state.get(key)
+        if cached is not None:
+            return cached
+        n = sum(p.numel() for p in run)
+        dev = run[0].device
+        m = torch.zeros(n, device=dev, dtype=torch.float32)
+        v = torch.zeros(n, device=dev, dtype=torch.float32)
+        off = 0
+        for p in run:
+            st = self.state[p]
+            k = p.numel()
+            if "exp_avg" in st:  # e.g. restored from a state_dict
+                m[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                v[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+            st["exp_avg"] = m[off:off + k].view(p.shape)
+            st["exp_avg_sq"] = v[off:off + k].view(p.shape)
+            st.setdefault("step", torch.zeros((), dtype=torch.float32))
+            off += k
+        self._flat_state[key] = (m, v)
+        return m, v
+
+    @torch.no_grad()
+    def step(self, closure=None, clip_groups=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        clip_of = {}
+        if clip_groups:
+            for plist, max_norm in clip_groups:
+                plist = [p for p in plist if p.grad is not None]
+                if not plist:
+                    continue
+                acc = grad_sumsq(plist)
+                for p in plist:
+                    clip_of[id(p)] = (acc, float(max_norm))
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            params = [p for p in group["params"] if p.grad is not None]
+            # runs must agree on memory layout AND on the clip group
+            runs = []
+            for run in _runs(params):
+                cur = [run[0]]
+                for p in run[1:]:
+                    if clip_of.get(id(p), (None,))[0] is clip_of.get(id(cur[0]), (None,))[0]:
+                        cur.append(p)
+                    else:
+                        runs.append(cur)
+                        cur = [p]
+                runs.append(cur)
+            for run in runs:
+                ops._check(run[0])
+                pflat = _contiguous_run(run)
+                if pflat is None or pflat.data_ptr() % 16:
+                    raise RuntimeError("FusedAdam: parameters must be fp32 ROCm tensors (NeRF flat buffers)")
+                gflat = _contiguous_run([p.grad for p in run])
+                copy_back = gflat is None or gflat.data_ptr() % 16
+                if copy_back:
+                    gflat = torch.cat([p.grad.reshape(-1) for p in run])
+                m, v = self._state_run(run)
+                st = self.state[run[0]]
+                st["step"] += 1
+                step = int(st["step"].item()) if st["step"].device.type == "cpu" else int(st["step"])
+                for p in run[1:]:
+                    self.state[p]["step"] = st["step"]
+                sumsq, max_norm = clip_of.get(id(run[0]), (None, 1.0))
+                ops.adam_step(pflat, gflat, m, v, group["lr"], b1, b2, group["eps"], step, sumsq=sumsq,
+                              max_norm=max_norm)
+                for p in run:  # parameters changed behind autograd's back: bump versions (NeRF repacks)
+                    torch.autograd.graph.increment_version(p)
+        return loss
