@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Benchmark of the NeRF training hot path on MI355X (BASELINE.json, config #2).
+
+One step = one reference training iteration (noisy_src/train.py:455-465):
+render coarse (64 stratified samples) + fine (128 inverse-CDF samples) for a
+batch of rays, MSE losses, backward through every HIP kernel, joint gradient
+clip, Adam, LambdaLR; with N GPUs the flat gradients are all-reduced over RCCL
+first.  Workload: lego 800x800 camera geometry (focal 1111.1, the 100 training
+poses of the reference's outputs/*/final_poses.pt fixture), 4096 rays per GPU
+per step (weak scaling), bf16 MFMA MLP with fp32 master weights.  The scene
+content is synthetic (random targets): the lego dataset is not available here.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision bf16|fp32]
+
+For N > 1 the driver runs it under torch.distributed.run (one rank per GPU).
+Rank 0 prints ONE JSON line.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path[:0] = [str(ROOT), str(ROOT / "robust-nerf_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "training rays/sec + test PSNR, lego 800² 64c+128f, at 1/2/4/8 MI355X"
+MACS_PER_EVAL = 593_408
+PEAK_TFLOPS = {"bf16": 2516.6, "fp32": 157.3}  # dense MFMA (256 CU x 2.4 GHz); MI355X_MICROARCH.md
+
+
+def lego_rays(n_rays: int, seed: int, device):
+    """Rays of the lego 800x800 training cameras (focal from camera_angle_x, data.py:147-150)."""
+    g = torch.Generator().manual_seed(seed)
+    fix = sorted((ROOT / "tests" / "golden").glob("final_poses_*.npz"))[0]
+    poses = torch.from_numpy(np.load(fix)["ground_truth_poses"])
+    H = W = 800
+    focal = 0.5 * W / math.tan(0.5 * 0.6911112070083618)
+    img = torch.randint(0, poses.shape[0], (n_rays,), generator=g)
+    i = torch.randint(0, W, (n_rays,), generator=g).float()
+    j = torch.randint(0, H, (n_rays,), generator=g).float()
+    dirs = torch.stack([(i - W / 2) / focal, -(j - H / 2) / focal, -torch.ones_like(i)], -1)
+    R = poses[img, :3, :3]
+    d = torch.einsum("bij,bj->bi", R, dirs)
+    d = d / d.norm(dim=-1, keepdim=True)
+    o = poses[img, :3, 3]
+    tgt = torch.rand(n_rays, 3, generator=g)
+    return o.to(device), d.to(device), tgt.to(device)
+
+
+def cpu_baseline(n_rays: int, steps: int):
+    """The oracle (torch CPU restatement of the reference) training step, 64c+128f."""
+    from types import SimpleNamespace
+
+    from oracle import refimpl as ref
+    torch.manual_seed(0)
+    rc = SimpleNamespace(near=2.0, far=6.0, num_samples=64, num_samples_fine=128, use_hierarchical=True,
+                         perturb=True, raw_noise_std=0.0, white_background=True)
+    mc, mf = ref.create_nerf()
+    state = ref.TrainState(mc, mf)
+    o, d, t = lego_rays(n_rays, 123, "cpu")
+    ref.train_step(mc, mf, state, o, d, t, rc)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ref.train_step(mc, mf, state, o, d, t, rc)
+    dt = time.perf_counter() - t0
+    return {"value": n_rays * steps / dt, "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle/refimpl.py train_step (fp32, torch CPU), {n_rays} rays x {steps} steps, "
+                      f"64c+128f, lego 800x800 camera rays; {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4096, help="rays per GPU per step")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--cpu-rays", type=int, default=1024)
+    ap.add_argument("--cpu-steps", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist.group.WORLD
+
+    from noisy_src import _hip
+    from noisy_src.config import ModelConfig, RenderConfig
+    from noisy_src.engine import Trainer
+    from noisy_src.model import create_nerf
+
+    torch.manual_seed(42)  # train.py:319 set_seed(42); identical init on every rank
+    mc, mf = create_nerf(ModelConfig(precision=args.precision))
+    mc, mf = mc.to(dev), mf.to(dev)
+    rcfg = RenderConfig()
+    trainer = Trainer(mc, mf, rcfg, process_group=pg)
+
+    B = args.batch
+    pool = [lego_rays(B, 1000 * rank + k, dev) for k in range(4)]
+    torch.manual_seed(1234 + rank)
+
+    def step(k):
+        o, d, t = pool[k % len(pool)]
+        return trainer.step(o, d, t)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+
+    timer = _hip.CallTimer(["nr_mlp_forward", "nr_mlp_backward"])
+    _hip.set_timer(timer)
+    if pg is not None:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        m = step(k)
+    torch.cuda.synchronize()
+    if pg is not None:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    _hip.set_timer(None)
+    loss = float(m["loss"])
+    if pg is not None:
+        tt = torch.tensor([dt], device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        dt = float(tt)
+
+    calls = timer.summary()
+    Mf = B * (rcfg.num_samples + rcfg.num_samples_fine)
+    key = f"nr_mlp_forward[M={Mf}]"
+    n_launch, ms = calls[key]
+    flops = 2.0 * MACS_PER_EVAL * Mf
+    peak = PEAK_TFLOPS[args.precision]
+    achieved = flops / (ms * 1e-3) / 1e12
+    value = world * B * args.steps / dt
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * dt / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (lego 800x800 camera rays from the reference's GT poses; random targets)",
+        "config": {
+            "workload": "lego 800x800 hierarchical 64c+128f training step, 4096 rays per GPU",
+            "global_batch": world * B,
+            "num_samples": rcfg.num_samples,
+            "num_samples_fine": rcfg.num_samples_fine,
+            "parallelism": f"dp{world}",
+        },
+        "roofline": {
+            "bound": "mfma",
+            "kernel": f"mlp_fwd_kernel (fine net, M={Mf} samples, training mode)",
+            "achieved": round(achieved, 2),
+            "peak": peak,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4),
+            "traffic": None,
+            "launch_ms": round(ms, 4),
+            "launches": n_launch,
+        },
+        "kernel_ms": {k: round(v[1], 4) for k, v in calls.items()},
+        "final_loss": round(loss, 6),
+        "psnr": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_rays, args.cpu_steps)
+    if rank == 0:
+        print(json.dumps(out))
+    if pg is not None:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -125,10 +125,43 @@ def stream_ptr(device: Optional[torch.device] = None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-def call(name: str, *args) -> int:
+class CallTimer:
+    """Brackets selected entry points with HIP events on the launching stream (the
+    current torch stream the kernels run on), for per-launch durations in bench.py."""
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.events = {}
+
+    def record(self, key, fn):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        rc = fn()
+        e.record()
+        self.events.setdefault(key, []).append((s, e))
+        return rc
+
+    def summary(self):
+        """key -> (launches, mean ms); call after torch.cuda.synchronize()."""
+        return {k: (len(v), sum(a.elapsed_time(b) for a, b in v) / len(v)) for k, v in self.events.items()}
+
+
+_timer: Optional[CallTimer] = None
+
+
+def set_timer(timer: Optional[CallTimer]) -> None:
+    global _timer
+    _timer = timer
+
+
+def call(name: str, *args, tag: str = "") -> int:
     """Invoke an ``nr_*`` entry point and raise RuntimeError on a non-zero code."""
     fn = getattr(load(), name)
-    rc = fn(*args)
+    if _timer is not None and name in _timer.names:
+        rc = _timer.record(f"{name}{tag}", lambda: fn(*args))
+    else:
+        rc = fn(*args)
     if isinstance(rc, int) and fn.restype is c_i and rc != 0:
         raise RuntimeError(f"{name} failed (code {rc}): {last_error()}")
     return rc

@@ -78,7 +78,7 @@ class _MLPFunction(torch.autograd.Function):
         if training and M > 0:
             saved = torch.empty(int(_hip.load().nr_mlp_saved_bytes(cfg, M)), device=xc.device, dtype=torch.uint8)
         call("nr_mlp_forward", cfg, ptr(packed), ptr(flat), ptr(xc), ptr(dc), M, ptr(rgb), ptr(sigma), ptr(saved),
-             _hip.stream_ptr())
+             _hip.stream_ptr(), tag=f"[M={M}]")
         if training:
             ctx.save_for_backward(xc, dc if dc is not None else xc.new_empty(0), rgb, sigma)
             ctx.has_d = dc is not None
@@ -101,7 +101,7 @@ class _MLPFunction(torch.autograd.Function):
             ws = torch.empty(int(_hip.load().nr_mlp_workspace_bytes(cfg, M)), device=dev, dtype=torch.uint8)
             call("nr_mlp_backward", cfg, ptr(packed), ptr(flat), ptr(xc), ptr(dc) if ctx.has_d else None, M, ptr(rgb),
                  ptr(sigma), ptr(saved), ptr(g_rgb), ptr(g_sigma), ptr(gflat), ptr(g_x), ptr(g_d), ptr(ws),
-                 _hip.stream_ptr())
+                 _hip.stream_ptr(), tag=f"[M={M}]")
         else:
             gflat.zero_()
         grads = []
