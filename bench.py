@@ -123,7 +123,7 @@ def main():
         step(k)
     torch.cuda.synchronize()
 
-    timer = _hip.CallTimer(["nr_mlp_forward", "nr_mlp_backward"])
+    timer = _hip.CallTimer(["nr_mlp_forward", "nr_mlp_backward_dx", "nr_mlp_backward_dw", "nr_mlp_backward_reduce"])
     _hip.set_timer(timer)
     if pg is not None:
         torch.distributed.barrier()

@@ -180,6 +180,22 @@ int nr_mlp_backward(const NrMlpConfig* cfg, const void* packed,
                     const float* g_sigma, float* g_params, float* g_x,
                     float* g_d, void* workspace, nr_stream_t stream);
 
+/* The three stages of nr_mlp_backward, callable separately (per-kernel timing):
+ * dx: dz of every layer into the workspace (+ g_x / g_d); dw: per-chunk dW/db
+ * slabs from the saved activations and dz; reduce: slabs -> g_params (chunk
+ * order, deterministic).  Same arguments and workspace as nr_mlp_backward. */
+int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed,
+                       const float* params, const float* x, const float* d,
+                       int64_t M, const float* rgb, const float* sigma,
+                       const void* saved, const float* g_rgb,
+                       const float* g_sigma, float* g_x, float* g_d,
+                       void* workspace, nr_stream_t stream);
+int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved,
+                       void* workspace, nr_stream_t stream);
+int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M,
+                           const void* workspace, float* g_params,
+                           nr_stream_t stream);
+
 /* ---- A13: optimizer tail  (noisy_src/train.py:112-117, train_pose_opt.py:398-409)
  * Sum of squares of n fp32 values added into *acc (device scalar, caller-zeroed). */
 int nr_sumsq(const float* x, int64_t n, float* acc, nr_stream_t stream);

@@ -5,16 +5,24 @@
 // trunk with skip cat([x_enc, h]) after layer 4, sigma = relu(W h), feat = W h
 // (no activation), h_c = relu(W [feat, d_enc]), rgb = sigmoid(W h_c).
 //
-// Formulation: every layer computes out^T = W . in^T with one 32-sample tile
-// per wave.  In the MFMA C/D layout a lane holds 16 features of ONE sample, so
-// a layer's accumulator tile is already the next layer's B operand (after a
-// pack to bf16, or as-is in fp32): activations stay in registers for the whole
-// network and never touch LDS.  The A operand (weights) comes from a packed
-// image in which each lane's 16 bytes for one MFMA are contiguous, with the
-// k order permuted to match the accumulator's row order:
+// Formulation.  Every layer computes out^T = W . in^T on 32-sample tiles.  In
+// the MFMA C/D layout a lane holds 16 features of ONE sample, so a layer's
+// accumulator tile is already the next layer's B operand (packed to bf16, or
+// as-is in fp32): activations stay in registers through the whole network.
+// The A operand (weights) is a packed image whose per-lane 16 bytes per MFMA
+// are contiguous, with the k order permuted to match the accumulator rows:
 //   bf16 32x32x16, k-step s: element j <-> input feature 16s + 8(j>>2) + 4h + (j&3)
 //   fp32 32x32x2,  k-step t: lane half h <-> input feature (t&3) + 8(t>>2) + 4h
-// The same images are built for W^T, so the backward chain has the same form.
+// The images are chunk-major (a chunk = all row blocks of one k block) and are
+// streamed through an LDS double buffer shared by the workgroup's 4 waves;
+// each wave applies every fragment to TPW sample tiles.
+//
+// Training saves activations (and the backward its dz) as B-operand images:
+// per tile and 32-feature block, FPB wave-wide 1-KB fragments, so each store
+// is one coalesced 1-KB wave write.  The dW GEMM reduces over samples, i.e.
+// over the lanes of those images; it stages whole tiles in LDS (LDS-DMA) and
+// rebuilds sample-major operands with the gfx950 transpose read
+// ds_read_b64_tr_b16 (bf16) or strided ds_read_b32 (fp32).
 #include <cstring>
 
 #include "common.hpp"
@@ -25,7 +33,8 @@
 
 namespace nr {
 
-constexpr int kWavesPerBlock = 4;
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
 
 template <int PREC>
 struct InBlk;
@@ -54,42 +63,15 @@ __device__ __forceinline__ void to_in(const f32x16& a, InBlk<PREC>& o) {
     }
 }
 
-// The flat nn.Module parameter layout has odd offsets (feature_linear starts at
-// 493,313 floats for the default model), so parameter reads are scalar.
-__device__ __forceinline__ f32x4 ld4u(const float* __restrict__ p) { return f32x4{p[0], p[1], p[2], p[3]}; }
-
 __device__ __forceinline__ void zero(f32x16& a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) a[r] = 0.f;
 }
 
-// acc[nb] += A(nb0+nb, kb0+kb) . in[kb]  for a packed image with KBtot column blocks.
-template <int PREC, int NBO, int KBN>
-__device__ __forceinline__ void gemm(f32x16 (&acc)[NBO], int nb0, const InBlk<PREC> (&in)[KBN], int kb0,
-                                     const char* __restrict__ base, int KBtot, int lane) {
-#pragma unroll
-    for (int kb = 0; kb < KBN; ++kb) {
-#pragma unroll
-        for (int nb = 0; nb < NBO; ++nb) {
-            const char* p = base + static_cast<int64_t>(((nb0 + nb) * KBtot + kb0 + kb) * kFPB<PREC>) * kFragBytes +
-                            lane * 16;
-            if constexpr (PREC == NR_PREC_BF16) {
-                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(p);
-                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(p + kFragBytes);
-                acc[nb] = mfma_bf16(a0, in[kb].s[0], acc[nb]);
-                acc[nb] = mfma_bf16(a1, in[kb].s[1], acc[nb]);
-            } else {
-#pragma unroll
-                for (int tq = 0; tq < 4; ++tq) {
-                    const f32x4 a = *reinterpret_cast<const f32x4*>(p + tq * kFragBytes);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) acc[nb] = mfma_f32(a[e], in[kb].v[4 * tq + e], acc[nb]);
-                }
-            }
-        }
-    }
-}
-
+#ifndef NR_SIN
+#define NR_SIN sinf
+#define NR_COS cosf
+#endif
 // Positional-encoding feature f of a 3-vector (model.py:72-80): [x | sin 2^0 x | cos 2^0 x | ...].
 __device__ __forceinline__ float pe_feat(float x0, float x1, float x2, int f, int L) {
     if (f < 3) return f == 0 ? x0 : (f == 1 ? x1 : x2);
@@ -100,10 +82,10 @@ __device__ __forceinline__ float pe_feat(float x0, float x1, float x2, int f, in
     const int c = rem % 3;
     const float xv = c == 0 ? x0 : (c == 1 ? x1 : x2);
     const float v = exp2f(static_cast<float>(k)) * xv;
-    return rem < 3 ? sinf(v) : cosf(v);
+    return rem < 3 ? NR_SIN(v) : NR_COS(v);
 }
 
-// d gamma_f / d x_c, contracted with g: adds into gx[c].
+// d gamma_f / d x_c contracted with g (torch: (g * cos(fx)) * f, (g * -sin(fx)) * f).
 __device__ __forceinline__ void pe_feat_bwd(float x0, float x1, float x2, int f, int L, float g, float& g0,
                                             float& g1, float& g2) {
     int c;
@@ -130,35 +112,60 @@ __device__ __forceinline__ void pe_feat_bwd(float x0, float x1, float x2, int f,
         g2 += d;
 }
 
-// Store one accumulator block (32 features x 32 samples) into a tile-blocked,
-// feature-major tensor: (f, m) at tile*F*32 + f*32 + m.
+// One 32-feature block of a tile as a B-operand image: FPB fragments of 1 KB.
 template <int PREC>
-__device__ __forceinline__ void store_block(char* __restrict__ region, int64_t tile, int F, int blk, const f32x16& v,
-                                            int lane) {
-    const int h = lane >> 5, ml = lane & 31;
-    const int64_t e0 = tile * F * 32 + static_cast<int64_t>(blk) * 32 * 32 + ml;
+__device__ __forceinline__ void store_img(char* __restrict__ region, int64_t tile, int nblk, int blk,
+                                          const InBlk<PREC>& v, int lane) {
+    char* base = region + ((tile * nblk + blk) * kFPB<PREC>) * static_cast<int64_t>(kFragBytes) + lane * 16;
+    if constexpr (PREC == NR_PREC_BF16) {
+        *reinterpret_cast<bf16x8*>(base) = v.s[0];
+        *reinterpret_cast<bf16x8*>(base + kFragBytes) = v.s[1];
+    } else {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int64_t e = e0 + acc_row(r, h) * 32;
-        if constexpr (PREC == NR_PREC_BF16)
-            reinterpret_cast<unsigned short*>(region)[e] = bf16_bits(v[r]);
-        else
-            reinterpret_cast<float*>(region)[e] = v[r];
+        for (int tq = 0; tq < 4; ++tq)
+            *reinterpret_cast<f32x4*>(base + tq * kFragBytes) =
+                f32x4{v.v[4 * tq], v.v[4 * tq + 1], v.v[4 * tq + 2], v.v[4 * tq + 3]};
     }
 }
 
-// bias + optional ReLU on NBO blocks; returns mask bits (bit nb*16+r) in w[4].
+template <int PREC>
+__device__ __forceinline__ void load_img(const char* __restrict__ region, int64_t tile, int nblk, int blk,
+                                         InBlk<PREC>& v, int lane) {
+    const char* base = region + ((tile * nblk + blk) * kFPB<PREC>) * static_cast<int64_t>(kFragBytes) + lane * 16;
+    if constexpr (PREC == NR_PREC_BF16) {
+        v.s[0] = *reinterpret_cast<const bf16x8*>(base);
+        v.s[1] = *reinterpret_cast<const bf16x8*>(base + kFragBytes);
+    } else {
+#pragma unroll
+        for (int tq = 0; tq < 4; ++tq) {
+            const f32x4 q = *reinterpret_cast<const f32x4*>(base + tq * kFragBytes);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v.v[4 * tq + e] = q[e];
+        }
+    }
+}
+
+// bias + optional ReLU on NBO blocks; mask bits (bit (nb&1)*16+r of word nb>>1) into w[4].
+// Vector images (mlp_plan.hpp): 16 fp32 per (block, lane half) in accumulator order.
+// The opaque lane-half copy keeps the compiler from hoisting these loads out of
+// the layer loops as invariants (they would then stay live, and spill).
+__device__ __forceinline__ const f32x4* vimg(const char* packed, int64_t off, int lane) {
+    int hl = lane >> 5;
+    asm volatile("" : "+v"(hl));
+    return reinterpret_cast<const f32x4*>(packed + off) + hl * 4;
+}
+// f32x4 g (registers 4g..4g+3) of block nb
+#define NR_VEC(img, nb, g) ((img)[(nb) * 8 + (g)])
+
 template <int NBO, bool RELU>
-__device__ __forceinline__ void bias_act(f32x16 (&acc)[NBO], const float* __restrict__ bias, int lane,
-                                         unsigned (&w)[4]) {
-    const int h = lane >> 5;
+__device__ __forceinline__ void bias_act(f32x16 (&acc)[NBO], const f32x4* __restrict__ bias, unsigned (&w)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) w[q] = 0u;
 #pragma unroll
     for (int nb = 0; nb < NBO; ++nb) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            const f32x4 b = ld4u(bias + 32 * nb + 8 * g + 4 * h);
+            const f32x4 b = NR_VEC(bias, nb, g);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int r = 4 * g + e;
@@ -171,6 +178,131 @@ __device__ __forceinline__ void bias_act(f32x16 (&acc)[NBO], const float* __rest
     }
 }
 
+template <int NBO>
+__device__ __forceinline__ void apply_mask(f32x16 (&acc)[NBO], u32x4 mw) {
+#pragma unroll
+    for (int nb = 0; nb < NBO; ++nb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const unsigned bit = (mw[nb >> 1] >> ((nb & 1) * 16 + r)) & 1u;
+            acc[nb][r] = bit ? acc[nb][r] : 0.f;
+        }
+}
+
+// ------------------------------------------------------ weight stream -----
+// A sequence of chunks (all row blocks of one k block of one layer image)
+// consumed in order through an LDS double buffer, register-staged one chunk
+// ahead: load(q+1) is issued before chunk q's MFMAs and written to the other
+// slot after them, then one barrier.  The slot written at step q was last read
+// at step q-1, which every wave finished before the previous barrier.
+constexpr int kMaxChunks = 176;  // >= sum of KB (forward) or NB (backward) over the MFMA layers
+
+struct StreamDesc {
+    int64_t base;                  // byte offset of the stream's first chunk in `packed`
+    int nq;                        // chunks
+    int ckb[kMaxChunks];           // chunk sizes in KB
+};
+
+struct Ring {
+    char* lds;
+    int slot_bytes;
+    int q;                         // chunk in the current slot
+    const char* src;               // next chunk to load
+};
+
+template <int G, int NT>
+struct Stager {
+    u32x4 v[G];
+
+    __device__ __forceinline__ void load(Ring& ring, const StreamDesc& sd, int q, int tid) {
+        if (q >= sd.nq) return;
+        const int bytes = sd.ckb[q] * 1024;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int b = (g * NT + tid) * 16;
+            if (b < bytes) v[g] = *reinterpret_cast<const u32x4*>(ring.src + b);
+        }
+        ring.src += bytes;
+    }
+
+    __device__ __forceinline__ void store(char* slot, const StreamDesc& sd, int q, int tid) {
+        if (q >= sd.nq) return;
+        const int bytes = sd.ckb[q] * 1024;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int b = (g * NT + tid) * 16;
+            if (b < bytes) *reinterpret_cast<u32x4*>(slot + b) = v[g];
+        }
+    }
+};
+
+// acc1[t][r] += A(row block nb0 + r) . in[t]   (r < N1)
+// acc2[t][r] += A(row block nb0 + N1 + r) . in[t]   (r < N2)
+// over KBN consecutive stream chunks (k blocks).
+template <int PREC, int TPW, int N1, int N2, int KBN, int G, int NT>
+__device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1],
+                                            f32x16 (&acc2)[TPW][N2 > 0 ? N2 : 1], int nb0,
+                                            const InBlk<PREC> (&in)[TPW][KBN], Ring& ring, Stager<G, NT>& st,
+                                            const char* __restrict__ packed, const StreamDesc& sd, int tid,
+                                            int lane) {
+#pragma unroll
+    for (int kb = 0; kb < KBN; ++kb) {
+        st.load(ring, sd, ring.q + 1, tid);
+        const char* slot = ring.lds + (ring.q & 1) * ring.slot_bytes + lane * 16;
+#pragma unroll
+        for (int r = 0; r < N1 + N2; ++r) {
+            const char* fp = slot + (nb0 + r) * kFPB<PREC> * kFragBytes;
+            constexpr int I1 = N1 > 0 ? N1 : 1;
+            constexpr int I2 = N2 > 0 ? N2 : 1;
+            const int r1 = r < N1 ? r : 0;
+            const int r2 = r >= N1 ? (r - N1) % I2 : 0;
+            (void)I1;
+            if constexpr (PREC == NR_PREC_BF16) {
+                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(fp);
+                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(fp + kFragBytes);
+#pragma unroll
+                for (int t = 0; t < TPW; ++t) {
+                    if (r < N1) {
+                        acc1[t][r1] = mfma_bf16(a0, in[t][kb].s[0], acc1[t][r1]);
+                        acc1[t][r1] = mfma_bf16(a1, in[t][kb].s[1], acc1[t][r1]);
+                    } else {
+                        acc2[t][r2] = mfma_bf16(a0, in[t][kb].s[0], acc2[t][r2]);
+                        acc2[t][r2] = mfma_bf16(a1, in[t][kb].s[1], acc2[t][r2]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int tq = 0; tq < 4; ++tq) {
+                    const f32x4 a = *reinterpret_cast<const f32x4*>(fp + tq * kFragBytes);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int t = 0; t < TPW; ++t) {
+                            if (r < N1)
+                                acc1[t][r1] = mfma_f32(a[e], in[t][kb].v[4 * tq + e], acc1[t][r1]);
+                            else
+                                acc2[t][r2] = mfma_f32(a[e], in[t][kb].v[4 * tq + e], acc2[t][r2]);
+                        }
+                }
+            }
+        }
+        st.store(ring.lds + ((ring.q + 1) & 1) * ring.slot_bytes, sd, ring.q + 1, tid);
+        __syncthreads();
+        ++ring.q;
+    }
+}
+
+template <int G, int NT>
+__device__ __forceinline__ void stream_begin(Ring& ring, Stager<G, NT>& st, const char* __restrict__ packed,
+                                             const StreamDesc& sd, int tid) {
+    ring.q = 0;
+    ring.src = packed + sd.base;
+    st.load(ring, sd, 0, tid);
+    st.store(ring.lds, sd, 0, tid);
+    __syncthreads();
+}
+
+// ------------------------------------------------------------ forward -----
 struct FwdArgs {
     const char* packed;
     const float* params;
@@ -182,156 +314,210 @@ struct FwdArgs {
     int64_t M, tiles;
     int L, Ld, n_layers;
     uint32_t skips;
-    int64_t pk[kMaxMfmaLayers];
-    int KB[kMaxMfmaLayers];
-    int64_t bias[kMaxMfmaLayers];
-    int64_t sig_w, sig_b, rgb_w, rgb_b;
+    int slot_bytes;
+    StreamDesc sd;  // W images: trunk 0..n-1, feat, dir
+    int64_t vb[kMaxMfmaLayers];
+    int64_t vsig, vrgb, sig_b, rgb_b;
     int64_t sv_off[kMaxTrunk + 4];
-    int sv_F[kMaxTrunk + 4];
     int sv_feat, sv_denc, sv_hc;
     int64_t mask_off;
     int n_mask;
 };
 
-template <int PREC, int XB, int DB, bool TRAIN>
-__global__ __launch_bounds__(64 * kWavesPerBlock) void mlp_fwd_kernel(FwdArgs a) {
-    const int lane = threadIdx.x & 63, h = lane >> 5, ml = lane & 31;
-    const int64_t tile = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
-    if (tile >= a.tiles) return;
-    const int64_t m = tile * 32 + ml;
-    const bool valid = m < a.M;
-    float x0 = 0.f, x1 = 0.f, x2 = 0.f;
-    if (valid) {
-        x0 = a.x[3 * m];
-        x1 = a.x[3 * m + 1];
-        x2 = a.x[3 * m + 2];
-    }
+template <int PREC, int XB, int DB, bool TRAIN, int TPW, int G, int NT>
+__global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ml = lane & 31;
+    const int64_t tile0 = (static_cast<int64_t>(blockIdx.x) * (NT / 64) + (tid >> 6)) * TPW;
     const int n = a.n_layers;
-    unsigned* masks = reinterpret_cast<unsigned*>(a.saved + a.mask_off);
-
-    InBlk<PREC> xe[XB];
+    float px[TPW][3];
+    bool tok[TPW];
 #pragma unroll
-    for (int kb = 0; kb < XB; ++kb) {
-        f32x16 t;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t[r] = pe_feat(x0, x1, x2, 32 * kb + acc_row(r, h), a.L);
-        to_in<PREC>(t, xe[kb]);
-        if constexpr (TRAIN) store_block<PREC>(a.saved + a.sv_off[SV_XENC], tile, a.sv_F[SV_XENC], kb, t, lane);
+    for (int t = 0; t < TPW; ++t) {
+        const int64_t m = (tile0 + t) * 32 + ml;
+        tok[t] = tile0 + t < a.tiles;
+        const bool valid = m < a.M;
+        px[t][0] = valid ? a.x[3 * m] : 0.f;
+        px[t][1] = valid ? a.x[3 * m + 1] : 0.f;
+        px[t][2] = valid ? a.x[3 * m + 2] : 0.f;
     }
+    u32x4* masks = reinterpret_cast<u32x4*>(a.saved + a.mask_off);
 
-    f32x16 acc[kHB];
-    InBlk<PREC> hin[kHB];
+    Ring ring{lds, a.slot_bytes, 0, nullptr};
+    Stager<G, NT> st;
+    stream_begin(ring, st, a.packed, a.sd, tid);
+
+    f32x16 acc[TPW][kHB];
+    InBlk<PREC> hin[TPW][kHB];
+    f32x16 dummy[TPW][1];
     unsigned w[4];
     for (int i = 0; i < n; ++i) {
 #pragma unroll
-        for (int nb = 0; nb < kHB; ++nb) zero(acc[nb]);
-        const char* base = a.packed + a.pk[i];
-        if (i == 0) {
-            gemm<PREC, kHB, XB>(acc, 0, xe, 0, base, a.KB[i], lane);
-        } else if ((a.skips >> (i - 1)) & 1u) {
-            gemm<PREC, kHB, XB>(acc, 0, xe, 0, base, a.KB[i], lane);
-            gemm<PREC, kHB, kHB>(acc, 0, hin, XB, base, a.KB[i], lane);
-        } else {
-            gemm<PREC, kHB, kHB>(acc, 0, hin, 0, base, a.KB[i], lane);
-        }
-        bias_act<kHB, true>(acc, a.params + a.bias[i], lane, w);
-        if constexpr (TRAIN) {
-            char* region = a.saved + a.sv_off[SV_H0 + i];
+        for (int t = 0; t < TPW; ++t)
 #pragma unroll
-            for (int nb = 0; nb < kHB; ++nb) store_block<PREC>(region, tile, kHidden, nb, acc[nb], lane);
-            reinterpret_cast<u32x4*>(masks)[(tile * a.n_mask + i) * 64 + lane] = u32x4{w[0], w[1], w[2], w[3]};
-        }
+            for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
+        const bool skip_in = i > 0 && ((a.skips >> (i - 1)) & 1u);
+        if (i == 0 || skip_in) {
+            // x_enc is not kept in registers: the skip layer reloads the saved
+            // copy (training) or recomputes it (inference)
+            InBlk<PREC> xe[TPW][XB];
 #pragma unroll
-        for (int nb = 0; nb < kHB; ++nb) to_in<PREC>(acc[nb], hin[nb]);
+            for (int t = 0; t < TPW; ++t) {
+                if (TRAIN && i > 0) {
+#pragma unroll
+                    for (int kb = 0; kb < XB; ++kb) {
+                        if (tok[t])
+                            load_img<PREC>(a.saved + a.sv_off[SV_XENC], tile0 + t, XB, kb, xe[t][kb], lane);
+                        else
+                            xe[t][kb] = InBlk<PREC>{};
+                    }
+                    continue;
+                }
+                // opaque copy: keeps the encoding from being hoisted out of the
+                // layer loop (and spilled) as a loop invariant
+                float p0 = px[t][0], p1 = px[t][1], p2 = px[t][2];
+                asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2));
+#pragma unroll
+                for (int kb = 0; kb < XB; ++kb) {
+                    f32x16 v;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) v[r] = pe_feat(p0, p1, p2, 32 * kb + acc_row(r, h), a.L);
+                    to_in<PREC>(v, xe[t][kb]);
+                    if constexpr (TRAIN)
+                        if (tok[t]) store_img<PREC>(a.saved + a.sv_off[SV_XENC], tile0 + t, XB, kb, xe[t][kb], lane);
+                }
+            }
+            stream_gemm<PREC, TPW, kHB, 0, XB, G, NT>(acc, dummy, 0, xe, ring, st, a.packed, a.sd, tid, lane);
+        }
+        if (i > 0) stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            bias_act<kHB, true>(acc[t], vimg(a.packed, a.vb[i], lane), w);
+#pragma unroll
+            for (int nb = 0; nb < kHB; ++nb) to_in<PREC>(acc[t][nb], hin[t][nb]);
+            if constexpr (TRAIN) {
+                if (tok[t]) {
+#pragma unroll
+                    for (int nb = 0; nb < kHB; ++nb)
+                        store_img<PREC>(a.saved + a.sv_off[SV_H0 + i], tile0 + t, kHB, nb, hin[t][nb], lane);
+                    masks[((tile0 + t) * a.n_mask + i) * 64 + lane] = u32x4{w[0], w[1], w[2], w[3]};
+                }
+            }
+        }
     }
 
-    // sigma head (VALU): relu(w_sigma . h + b)
-    float sp = 0.f;
+    // sigma head (VALU): relu(w_sigma . h + b), from the fp32 activations
+    float sp[TPW];
     {
-        const float* ws = a.params + a.sig_w;
+        const f32x4* ws = vimg(a.packed, a.vsig, lane);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) sp[t] = 0.f;
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const f32x4 wv = ld4u(ws + 32 * nb + 8 * g + 4 * h);
+                const f32x4 wv = NR_VEC(ws, nb, g);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) sp += wv[e] * acc[nb][4 * g + e];
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int t = 0; t < TPW; ++t) sp[t] += wv[e] * acc[t][nb][4 * g + e];
             }
-        sp += __shfl_xor(sp, 32);
-        sp = sp + a.params[a.sig_b];
-        sp = sp > 0.f ? sp : 0.f;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            sp[t] += __shfl_xor(sp[t], 32);
+            sp[t] = sp[t] + a.params[a.sig_b];
+            sp[t] = sp[t] > 0.f ? sp[t] : 0.f;
+        }
     }
 
     // feature_linear (no activation)
 #pragma unroll
-    for (int nb = 0; nb < kHB; ++nb) zero(acc[nb]);
-    gemm<PREC, kHB, kHB>(acc, 0, hin, 0, a.packed + a.pk[n], a.KB[n], lane);
-    bias_act<kHB, false>(acc, a.params + a.bias[n], lane, w);
-    if constexpr (TRAIN) {
+    for (int t = 0; t < TPW; ++t)
 #pragma unroll
-        for (int nb = 0; nb < kHB; ++nb) store_block<PREC>(a.saved + a.sv_off[a.sv_feat], tile, kHidden, nb, acc[nb], lane);
+        for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
+    stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[n], lane), w);
+#pragma unroll
+        for (int nb = 0; nb < kHB; ++nb) {
+            to_in<PREC>(acc[t][nb], hin[t][nb]);
+            if constexpr (TRAIN)
+                if (tok[t]) store_img<PREC>(a.saved + a.sv_off[a.sv_feat], tile0 + t, kHB, nb, hin[t][nb], lane);
+        }
     }
-#pragma unroll
-    for (int nb = 0; nb < kHB; ++nb) to_in<PREC>(acc[nb], hin[nb]);
 
     // dir_linear over [feat, d_enc], ReLU
     constexpr int NC = kHB / 2;
-    f32x16 ac[NC];
+    f32x16 ac[TPW][NC];
 #pragma unroll
-    for (int nb = 0; nb < NC; ++nb) zero(ac[nb]);
-    const char* dbase = a.packed + a.pk[n + 1];
-    gemm<PREC, NC, kHB>(ac, 0, hin, 0, dbase, a.KB[n + 1], lane);
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int nb = 0; nb < NC; ++nb) zero(ac[t][nb]);
+    stream_gemm<PREC, TPW, NC, 0, kHB, G, NT>(ac, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane);
     if constexpr (DB > 0) {
-        float d0 = 0.f, d1 = 0.f, d2 = 0.f;
-        if (valid) {
-            d0 = a.d[3 * m];
-            d1 = a.d[3 * m + 1];
-            d2 = a.d[3 * m + 2];
-        }
-        InBlk<PREC> de[DB];
+        InBlk<PREC> de[TPW][DB];
 #pragma unroll
-        for (int kb = 0; kb < DB; ++kb) {
-            f32x16 t;
+        for (int t = 0; t < TPW; ++t) {
+            const int64_t m = (tile0 + t) * 32 + ml;
+            const bool valid = m < a.M;
+            const float d0 = valid ? a.d[3 * m] : 0.f, d1 = valid ? a.d[3 * m + 1] : 0.f,
+                        d2 = valid ? a.d[3 * m + 2] : 0.f;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) t[r] = pe_feat(d0, d1, d2, 32 * kb + acc_row(r, h), a.Ld);
-            to_in<PREC>(t, de[kb]);
-            if constexpr (TRAIN) store_block<PREC>(a.saved + a.sv_off[a.sv_denc], tile, DB * 32, kb, t, lane);
-        }
-        gemm<PREC, NC, DB>(ac, 0, de, kHB, dbase, a.KB[n + 1], lane);
-    }
-    bias_act<NC, true>(ac, a.params + a.bias[n + 1], lane, w);
-    if constexpr (TRAIN) {
+            for (int kb = 0; kb < DB; ++kb) {
+                f32x16 v;
 #pragma unroll
-        for (int nb = 0; nb < NC; ++nb) store_block<PREC>(a.saved + a.sv_off[a.sv_hc], tile, kHidden / 2, nb, ac[nb], lane);
-        reinterpret_cast<u32x4*>(masks)[(tile * a.n_mask + n) * 64 + lane] = u32x4{w[0], w[1], w[2], w[3]};
-    }
-
-    // rgb head (VALU): sigmoid(W_rgb h_c + b)
-    float pr[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const float* wr = a.params + a.rgb_w + c * (kHidden / 2);
-        float s = 0.f;
-#pragma unroll
-        for (int nb = 0; nb < NC; ++nb)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 wv = ld4u(wr + 32 * nb + 8 * g + 4 * h);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) s += wv[e] * ac[nb][4 * g + e];
+                for (int r = 0; r < 16; ++r) v[r] = pe_feat(d0, d1, d2, 32 * kb + acc_row(r, h), a.Ld);
+                to_in<PREC>(v, de[t][kb]);
+                if constexpr (TRAIN)
+                    if (tok[t]) store_img<PREC>(a.saved + a.sv_off[a.sv_denc], tile0 + t, DB, kb, de[t][kb], lane);
             }
-        s += __shfl_xor(s, 32);
-        s = s + a.params[a.rgb_b + c];
-        pr[c] = 1.0f / (1.0f + expf(-s));
+        }
+        stream_gemm<PREC, TPW, NC, 0, DB, G, NT>(ac, dummy, 0, de, ring, st, a.packed, a.sd, tid, lane);
     }
-    if (valid && h == 0) {
-        a.rgb[3 * m] = pr[0];
-        a.rgb[3 * m + 1] = pr[1];
-        a.rgb[3 * m + 2] = pr[2];
-        a.sigma[m] = sp;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        bias_act<NC, true>(ac[t], vimg(a.packed, a.vb[n + 1], lane), w);
+        if constexpr (TRAIN) {
+            if (tok[t]) {
+#pragma unroll
+                for (int nb = 0; nb < NC; ++nb) {
+                    InBlk<PREC> v;
+                    to_in<PREC>(ac[t][nb], v);
+                    store_img<PREC>(a.saved + a.sv_off[a.sv_hc], tile0 + t, NC, nb, v, lane);
+                }
+                masks[((tile0 + t) * a.n_mask + n) * 64 + lane] = u32x4{w[0], w[1], w[2], w[3]};
+            }
+        }
+        // rgb head (VALU): sigmoid(W_rgb h_c + b)
+        float pr[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const f32x4* wr = vimg(a.packed, a.vrgb, lane) + c * NC * 8;
+            float s = 0.f;
+#pragma unroll
+            for (int nb = 0; nb < NC; ++nb)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 wv = NR_VEC(wr, nb, g);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) s += wv[e] * ac[t][nb][4 * g + e];
+                }
+            s += __shfl_xor(s, 32);
+            s = s + a.params[a.rgb_b + c];
+            pr[c] = 1.0f / (1.0f + expf(-s));
+        }
+        const int64_t m = (tile0 + t) * 32 + ml;
+        if (m < a.M && h == 0) {
+            a.rgb[3 * m] = pr[0];
+            a.rgb[3 * m + 1] = pr[1];
+            a.rgb[3 * m + 2] = pr[2];
+            a.sigma[m] = sp[t];
+        }
     }
 }
 
+// ----------------------------------------------------------- backward -----
 struct BwdArgs {
     const char* packed;
     const float* params;
@@ -348,263 +534,309 @@ struct BwdArgs {
     int64_t M, tiles;
     int L, Ld, n_layers;
     uint32_t skips;
-    int64_t pkT[kMaxMfmaLayers];
-    int NB[kMaxMfmaLayers];
-    int64_t sig_w, rgb_w;
+    int slot_bytes;
+    StreamDesc sd;  // W^T images: dir, feat, trunk n-1..1 [, trunk 0 when g_x/g_d]
+    int64_t vsig, vrgb;
     int64_t mask_off;
     int n_mask;
     int64_t ws_off[kMaxTrunk + 3];
     int ws_feat, ws_dir, ws_heads;
 };
 
-template <int NBO>
-__device__ __forceinline__ void apply_mask(f32x16 (&acc)[NBO], u32x4 mw) {
-#pragma unroll
-    for (int nb = 0; nb < NBO; ++nb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const unsigned bit = (mw[nb >> 1] >> ((nb & 1) * 16 + r)) & 1u;
-            acc[nb][r] = bit ? acc[nb][r] : 0.f;
-        }
-}
-
-template <int PREC, int XB, int DB>
-__global__ __launch_bounds__(64 * kWavesPerBlock) void mlp_bwd_kernel(BwdArgs a) {
-    const int lane = threadIdx.x & 63, h = lane >> 5, ml = lane & 31;
-    const int64_t tile = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
-    if (tile >= a.tiles) return;
-    const int64_t m = tile * 32 + ml;
-    const bool valid = m < a.M;
+template <int PREC, int XB, int DB, int TPW, int G, int NT, bool WANT_X>
+__global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ml = lane & 31;
+    const int64_t tile0 = (static_cast<int64_t>(blockIdx.x) * (NT / 64) + (tid >> 6)) * TPW;
     const int n = a.n_layers;
     const u32x4* masks = reinterpret_cast<const u32x4*>(a.saved + a.mask_off);
-    auto mask_of = [&](int layer) { return masks[(tile * a.n_mask + layer) * 64 + lane]; };
+    bool tok[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) tok[t] = tile0 + t < a.tiles;
+    auto mask_of = [&](int t, int layer) -> u32x4 {
+        return tok[t] ? masks[((tile0 + t) * a.n_mask + layer) * 64 + lane] : u32x4{0u, 0u, 0u, 0u};
+    };
+
+    Ring ring{lds, a.slot_bytes, 0, nullptr};
+    Stager<G, NT> st;
+    stream_begin(ring, st, a.packed, a.sd, tid);
 
     // heads: sigmoid / relu backward (torch: g * (1 - y) * y ; g * (y > 0))
-    float dz_rgb[3] = {0.f, 0.f, 0.f}, dz_s = 0.f;
-    if (valid) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float y = a.rgb[3 * m + c];
-            dz_rgb[c] = (a.g_rgb[3 * m + c] * (1.0f - y)) * y;
-        }
-        dz_s = a.sigma[m] > 0.f ? a.g_sigma[m] : 0.f;
-    }
-    {
-        f32x16 hb;
-        zero(hb);
-        if (h == 0) {
-            hb[0] = dz_s;
-            hb[1] = dz_rgb[0];
-            hb[2] = dz_rgb[1];
-            hb[3] = dz_rgb[2];
-        }
-        store_block<PREC>(a.ws + a.ws_off[a.ws_heads], tile, 32, 0, hb, lane);
-    }
-
-    // dz_c = (W_rgb^T dz_rgb) * [h_c > 0]
     constexpr int NC = kHB / 2;
-    f32x16 dc[NC];
-    {
-        const float* wr = a.params + a.rgb_w;
+    float dzs[TPW];
+    InBlk<PREC> cin[TPW][NC];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int64_t m = (tile0 + t) * 32 + ml;
+        const bool valid = m < a.M;
+        float dr[3] = {0.f, 0.f, 0.f};
+        dzs[t] = 0.f;
+        if (valid) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float y = a.rgb[3 * m + c];
+                dr[c] = (a.g_rgb[3 * m + c] * (1.0f - y)) * y;
+            }
+            dzs[t] = a.sigma[m] > 0.f ? a.g_sigma[m] : 0.f;
+        }
+        if (tok[t]) {
+            // dz of the heads as one 32-feature block: feature 0 sigma, 1..3 rgb
+            f32x16 hb;
+            zero(hb);
+            if (h == 0) {
+                hb[0] = dzs[t];
+                hb[1] = dr[0];
+                hb[2] = dr[1];
+                hb[3] = dr[2];
+            }
+            InBlk<PREC> hv;
+            to_in<PREC>(hb, hv);
+            store_img<PREC>(a.ws + a.ws_off[a.ws_heads], tile0 + t, 1, 0, hv, lane);
+        }
+        // dz_c = (W_rgb^T dz_rgb) * [h_c > 0]
+        f32x16 dc[NC];
+        const f32x4* wr = vimg(a.packed, a.vrgb, lane);
 #pragma unroll
         for (int nb = 0; nb < NC; ++nb)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const int f0 = 32 * nb + 8 * g + 4 * h;
-                const f32x4 w0 = ld4u(wr + f0);
-                const f32x4 w1 = ld4u(wr + kHidden / 2 + f0);
-                const f32x4 w2 = ld4u(wr + kHidden + f0);
+                const f32x4 w0 = NR_VEC(wr, nb, g), w1 = NR_VEC(wr + NC * 8, nb, g), w2 = NR_VEC(wr + 2 * NC * 8, nb, g);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) dc[nb][4 * g + e] = (w0[e] * dz_rgb[0] + w1[e] * dz_rgb[1]) + w2[e] * dz_rgb[2];
+                for (int e = 0; e < 4; ++e) dc[nb][4 * g + e] = (w0[e] * dr[0] + w1[e] * dr[1]) + w2[e] * dr[2];
             }
-        apply_mask<NC>(dc, mask_of(n));
-    }
-    InBlk<PREC> cin[NC];
+        apply_mask<NC>(dc, mask_of(t, n));
 #pragma unroll
-    for (int nb = 0; nb < NC; ++nb) {
-        store_block<PREC>(a.ws + a.ws_off[a.ws_dir], tile, kHidden / 2, nb, dc[nb], lane);
-        to_in<PREC>(dc[nb], cin[nb]);
+        for (int nb = 0; nb < NC; ++nb) {
+            to_in<PREC>(dc[nb], cin[t][nb]);
+            if (tok[t]) store_img<PREC>(a.ws + a.ws_off[a.ws_dir], tile0 + t, NC, nb, cin[t][nb], lane);
+        }
     }
 
-    // d feat = W_dir^T dz_c  (feature_linear has no activation: dz_feat = d feat)
-    f32x16 acc[kHB];
-    InBlk<PREC> hin[kHB];
+    // d [feat | d_enc] = W_dir^T dz_c   (feature_linear has no activation: dz_feat = d feat)
+    f32x16 acc[TPW][kHB];
+    InBlk<PREC> hin[TPW][kHB];
 #pragma unroll
-    for (int nb = 0; nb < kHB; ++nb) zero(acc[nb]);
-    const char* dirT = a.packed + a.pkT[n + 1];
-    gemm<PREC, kHB, NC>(acc, 0, cin, 0, dirT, a.NB[n + 1], lane);
-    if constexpr (DB > 0) {
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
+    constexpr int DBX = (WANT_X && DB > 0) ? DB : 0;
+    f32x16 dd[TPW][DBX > 0 ? DBX : 1];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int k = 0; k < (DBX > 0 ? DBX : 1); ++k) zero(dd[t][k]);
+    stream_gemm<PREC, TPW, kHB, DBX, NC, G, NT>(acc, dd, 0, cin, ring, st, a.packed, a.sd, tid, lane);
+    if constexpr (DBX > 0) {
         if (a.g_d) {
-            f32x16 dd[DB];
 #pragma unroll
-            for (int kb = 0; kb < DB; ++kb) zero(dd[kb]);
-            gemm<PREC, DB, NC>(dd, kHB, cin, 0, dirT, a.NB[n + 1], lane);
-            float d0 = 0.f, d1 = 0.f, d2 = 0.f;
-            if (valid) {
-                d0 = a.d[3 * m];
-                d1 = a.d[3 * m + 1];
-                d2 = a.d[3 * m + 2];
-            }
-            float g0 = 0.f, g1 = 0.f, g2 = 0.f;
+            for (int t = 0; t < TPW; ++t) {
+                const int64_t m = (tile0 + t) * 32 + ml;
+                const bool valid = m < a.M;
+                const float d0 = valid ? a.d[3 * m] : 0.f, d1 = valid ? a.d[3 * m + 1] : 0.f,
+                            d2 = valid ? a.d[3 * m + 2] : 0.f;
+                float g0 = 0.f, g1 = 0.f, g2 = 0.f;
 #pragma unroll
-            for (int kb = 0; kb < DB; ++kb)
+                for (int kb = 0; kb < DBX; ++kb)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) pe_feat_bwd(d0, d1, d2, 32 * kb + acc_row(r, h), a.Ld, dd[kb][r], g0, g1, g2);
-            g0 += __shfl_xor(g0, 32);
-            g1 += __shfl_xor(g1, 32);
-            g2 += __shfl_xor(g2, 32);
-            if (valid && h == 0) {
-                a.g_d[3 * m] = g0;
-                a.g_d[3 * m + 1] = g1;
-                a.g_d[3 * m + 2] = g2;
+                    for (int r = 0; r < 16; ++r)
+                        pe_feat_bwd(d0, d1, d2, 32 * kb + acc_row(r, h), a.Ld, dd[t][kb][r], g0, g1, g2);
+                g0 += __shfl_xor(g0, 32);
+                g1 += __shfl_xor(g1, 32);
+                g2 += __shfl_xor(g2, 32);
+                if (valid && h == 0) {
+                    a.g_d[3 * m] = g0;
+                    a.g_d[3 * m + 1] = g1;
+                    a.g_d[3 * m + 2] = g2;
+                }
             }
         }
     }
 #pragma unroll
-    for (int nb = 0; nb < kHB; ++nb) {
-        store_block<PREC>(a.ws + a.ws_off[a.ws_feat], tile, kHidden, nb, acc[nb], lane);
-        to_in<PREC>(acc[nb], hin[nb]);
-    }
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int nb = 0; nb < kHB; ++nb) {
+            to_in<PREC>(acc[t][nb], hin[t][nb]);
+            if (tok[t]) store_img<PREC>(a.ws + a.ws_off[a.ws_feat], tile0 + t, kHB, nb, hin[t][nb], lane);
+        }
 
     // d h_{n-1} = W_feat^T dz_feat + w_sigma dz_sigma, then * [h_{n-1} > 0]
+    f32x16 dummy[TPW][1];
 #pragma unroll
-    for (int nb = 0; nb < kHB; ++nb) zero(acc[nb]);
-    gemm<PREC, kHB, kHB>(acc, 0, hin, 0, a.packed + a.pkT[n], a.NB[n], lane);
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
+    stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane);
     {
-        const float* ws = a.params + a.sig_w;
+        const f32x4* ws = vimg(a.packed, a.vsig, lane);
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const f32x4 wv = ld4u(ws + 32 * nb + 8 * g + 4 * h);
+                const f32x4 wv = NR_VEC(ws, nb, g);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) acc[nb][4 * g + e] = acc[nb][4 * g + e] + wv[e] * dz_s;
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int t = 0; t < TPW; ++t) acc[t][nb][4 * g + e] = acc[t][nb][4 * g + e] + wv[e] * dzs[t];
             }
     }
-    apply_mask<kHB>(acc, mask_of(n - 1));
 #pragma unroll
-    for (int nb = 0; nb < kHB; ++nb) {
-        store_block<PREC>(a.ws + a.ws_off[WS_DZ0 + n - 1], tile, kHidden, nb, acc[nb], lane);
-        to_in<PREC>(acc[nb], hin[nb]);
-    }
-
-    // trunk: dz_{i-1} = (W_i^T dz_i)[h part] * [h_{i-1} > 0]
-    f32x16 dxe[XB];
-#pragma unroll
-    for (int kb = 0; kb < XB; ++kb) zero(dxe[kb]);
-    const bool want_x = a.g_x != nullptr;
-    for (int i = n - 1; i >= 1; --i) {
-        const char* baseT = a.packed + a.pkT[i];
-#pragma unroll
-        for (int nb = 0; nb < kHB; ++nb) zero(acc[nb]);
-        if ((a.skips >> (i - 1)) & 1u) {
-            if (want_x) gemm<PREC, XB, kHB>(dxe, 0, hin, 0, baseT, a.NB[i], lane);
-            gemm<PREC, kHB, kHB>(acc, XB, hin, 0, baseT, a.NB[i], lane);
-        } else {
-            gemm<PREC, kHB, kHB>(acc, 0, hin, 0, baseT, a.NB[i], lane);
-        }
-        apply_mask<kHB>(acc, mask_of(i - 1));
+    for (int t = 0; t < TPW; ++t) {
+        apply_mask<kHB>(acc[t], mask_of(t, n - 1));
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb) {
-            store_block<PREC>(a.ws + a.ws_off[WS_DZ0 + i - 1], tile, kHidden, nb, acc[nb], lane);
-            to_in<PREC>(acc[nb], hin[nb]);
+            to_in<PREC>(acc[t][nb], hin[t][nb]);
+            if (tok[t]) store_img<PREC>(a.ws + a.ws_off[WS_DZ0 + n - 1], tile0 + t, kHB, nb, hin[t][nb], lane);
         }
     }
-    if (want_x) {
-        gemm<PREC, XB, kHB>(dxe, 0, hin, 0, a.packed + a.pkT[0], a.NB[0], lane);
-        float x0 = 0.f, x1 = 0.f, x2 = 0.f;
-        if (valid) {
-            x0 = a.x[3 * m];
-            x1 = a.x[3 * m + 1];
-            x2 = a.x[3 * m + 2];
+
+    // trunk: dz_{i-1} = (W_i^T dz_i)[h rows] * [h_{i-1} > 0]; x_enc rows feed g_x
+    constexpr int XBX = WANT_X ? XB : 0;
+    f32x16 dxe[TPW][XBX > 0 ? XBX : 1];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int k = 0; k < (XBX > 0 ? XBX : 1); ++k) zero(dxe[t][k]);
+    for (int i = n - 1; i >= 1; --i) {
+#pragma unroll
+        for (int t = 0; t < TPW; ++t)
+#pragma unroll
+            for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
+        if ((a.skips >> (i - 1)) & 1u) {
+            if constexpr (XBX > 0)
+                stream_gemm<PREC, TPW, XBX, kHB, kHB, G, NT>(dxe, acc, 0, hin, ring, st, a.packed, a.sd, tid, lane);
+            else
+                stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, XB, hin, ring, st, a.packed, a.sd, tid, lane);
+        } else {
+            stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane);
         }
-        float g0 = 0.f, g1 = 0.f, g2 = 0.f;
 #pragma unroll
-        for (int kb = 0; kb < XB; ++kb)
+        for (int t = 0; t < TPW; ++t) {
+            apply_mask<kHB>(acc[t], mask_of(t, i - 1));
 #pragma unroll
-            for (int r = 0; r < 16; ++r) pe_feat_bwd(x0, x1, x2, 32 * kb + acc_row(r, h), a.L, dxe[kb][r], g0, g1, g2);
-        g0 += __shfl_xor(g0, 32);
-        g1 += __shfl_xor(g1, 32);
-        g2 += __shfl_xor(g2, 32);
-        if (valid && h == 0) {
-            a.g_x[3 * m] = g0;
-            a.g_x[3 * m + 1] = g1;
-            a.g_x[3 * m + 2] = g2;
+            for (int nb = 0; nb < kHB; ++nb) {
+                to_in<PREC>(acc[t][nb], hin[t][nb]);
+                if (tok[t]) store_img<PREC>(a.ws + a.ws_off[WS_DZ0 + i - 1], tile0 + t, kHB, nb, hin[t][nb], lane);
+            }
+        }
+    }
+    if constexpr (XBX > 0) {
+        stream_gemm<PREC, TPW, XBX, 0, kHB, G, NT>(dxe, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane);
+        if (a.g_x) {
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                const int64_t m = (tile0 + t) * 32 + ml;
+                const bool valid = m < a.M;
+                const float x0 = valid ? a.x[3 * m] : 0.f, x1 = valid ? a.x[3 * m + 1] : 0.f,
+                            x2 = valid ? a.x[3 * m + 2] : 0.f;
+                float g0 = 0.f, g1 = 0.f, g2 = 0.f;
+#pragma unroll
+                for (int kb = 0; kb < XBX; ++kb)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        pe_feat_bwd(x0, x1, x2, 32 * kb + acc_row(r, h), a.L, dxe[t][kb][r], g0, g1, g2);
+                g0 += __shfl_xor(g0, 32);
+                g1 += __shfl_xor(g1, 32);
+                g2 += __shfl_xor(g2, 32);
+                if (valid && h == 0) {
+                    a.g_x[3 * m] = g0;
+                    a.g_x[3 * m + 1] = g1;
+                    a.g_x[3 * m + 2] = g2;
+                }
+            }
         }
     }
 }
 
 // ------------------------------------------------------------------ dW ----
-// slab[job][chunk][row][col] += sum over the chunk's tiles of dz[row] x in[col];
-// column KB*32 of each row holds the bias partial sum_m dz[row].
+// Workgroup = (job, chunk of tiles, group of up to 4 sub-grids of 4x4 blocks).
+// Per tile the job's dz and input blocks are staged in LDS (double buffered,
+// LDS-DMA in 1-KB wave pieces); each wave accumulates its sub-grid with
+// operands rebuilt sample-major from the B-operand images.  Output slab per
+// chunk: [dz row][input col | bias] fp32.
 struct DwArgs {
     const char* saved;
     const char* ws;
     float* slabs;
     int64_t tiles;
-    int chunks, tiles_per_chunk;
+    int tiles_per_chunk;
     int n_jobs;
-    int job_wg0[kMaxJobs + 1];  // first workgroup of each job (cumulative)
-    int job_sg[kMaxJobs];        // 4x4-block subgrids per job
-    int job_nbg[kMaxJobs];       // subgrid rows (ceil(NB/4))
-    int job_NB[kMaxJobs], job_KB[kMaxJobs], job_row0[kMaxJobs];
-    int job_nin[kMaxJobs];
-    int64_t job_dz_off[kMaxJobs];  // bytes
-    int job_dz_F[kMaxJobs];
-    int64_t job_in_off[kMaxJobs][kMaxSeg];
-    int job_in_F[kMaxJobs][kMaxSeg];
-    int job_in_blocks[kMaxJobs][kMaxSeg];
-    int64_t job_slab[kMaxJobs];    // floats
+    int stage_bytes;
+    int job_wg0[kMaxJobs + 1];
+    int job_sg[kMaxJobs], job_nbg[kMaxJobs], job_groups[kMaxJobs];
+    int job_NBz[kMaxJobs], job_KB[kMaxJobs];
+    int job_nseg[kMaxJobs];                   // dz segments then input segments
+    int64_t seg_off[kMaxJobs][2 * kMaxSeg];   // byte offset of the tensor region
+    int seg_blocks[kMaxJobs][2 * kMaxSeg];
+    int seg_isws[kMaxJobs][2 * kMaxSeg];
+    int64_t job_slab[kMaxJobs];
     int64_t slab_floats_per_chunk;
 };
 
-// Operand fragment of a tile-blocked feature-major tensor for reduction over samples.
-// bf16 32x32x16: lane (row i, half h), k-step s: 8 samples 16s+8h .. +7 of feature row.
-template <int PREC>
-__device__ __forceinline__ void load_rowfrag(const char* __restrict__ region, int64_t tile, int F, int row, int lane,
-                                             bf16x8 (&b)[2], f32x4 (&f)[4]) {
-    const int h = lane >> 5, i = lane & 31;
-    if constexpr (PREC == NR_PREC_BF16) {
-        const __bf16* p = reinterpret_cast<const __bf16*>(region) + (tile * F + row + i) * 32 + 8 * h;
-        b[0] = *reinterpret_cast<const bf16x8*>(p);
-        b[1] = *reinterpret_cast<const bf16x8*>(p + 16);
-    } else {
-        const float* p = reinterpret_cast<const float*>(region) + (tile * F + row + i) * 32 + 16 * h;
+// Block-local feature of dW operand row/col index r: r = 16h + i <-> accumulator
+// register i of lane half h in the B-operand image.
+__device__ __forceinline__ int dw_feat(int r) { return acc_row(r & 15, r >> 4); }
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// bf16 operand of k-step ks (16 samples) from a staged block image [s][L][8]:
+// lane l = 16g + i (h = g&1, hh = g>>1) receives feature acc_row(i, h) of
+// samples 16ks + 8hh + 0..7, via two transpose reads of 4 samples x 16 features
+// (lane 4q+p of the group addresses sample q, features 4p..4p+3, cdna_hip T10).
+__device__ __forceinline__ bf16x8 dw_frag_bf16(const char* blk, int ks, int lane) {
+    const int g = lane >> 4, h = g & 1, hh = g >> 1;
+    const int lam = lane & 15, q = lam >> 2, p = lam & 3;
+    const int s = p >> 1;
+    const int m0 = 16 * ks + 8 * hh + q;
+    const char* a0 = blk + (s * 64 + m0 + 32 * h) * 16 + 8 * (p & 1);
+    const char* a1 = a0 + 4 * 16;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+    bf16x8 r;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) f[q] = *reinterpret_cast<const f32x4*>(p + 4 * q);
+    for (int j = 0; j < 4; ++j) {
+        r[j] = __builtin_bit_cast(__bf16, lo[j]);
+        r[4 + j] = __builtin_bit_cast(__bf16, hi[j]);
     }
+    return r;
 }
 
 template <int PREC>
-__global__ __launch_bounds__(64 * kWavesPerBlock) void mlp_dw_kernel(DwArgs a) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+__global__ __launch_bounds__(kThreads, 1) void mlp_dw_kernel(DwArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wg = blockIdx.x;
     int j = 0;
     while (j + 1 < a.n_jobs && wg >= a.job_wg0[j + 1]) ++j;
-    const int per_chunk = (a.job_sg[j] + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int groups = a.job_groups[j];
     const int local = wg - a.job_wg0[j];
-    const int chunk = local / per_chunk;
-    const int sg = (local % per_chunk) * kWavesPerBlock + wv;
-    if (sg >= a.job_sg[j]) return;
-    const int nbg = sg % a.job_nbg[j], kbg = sg / a.job_nbg[j];
-    const int NB = a.job_NB[j], KB = a.job_KB[j];
+    const int chunk = local / groups;
+    const int sg = (local % groups) * kWaves + wv;
+    const bool active = sg < a.job_sg[j];
+    const int nbg = active ? sg % a.job_nbg[j] : 0, kbg = active ? sg / a.job_nbg[j] : 0;
+    const int NBz = a.job_NBz[j], KB = a.job_KB[j];
     const int64_t t0 = static_cast<int64_t>(chunk) * a.tiles_per_chunk;
     int64_t t1 = t0 + a.tiles_per_chunk;
     if (t1 > a.tiles) t1 = a.tiles;
+    constexpr int FPB = kFPB<PREC>;
+    constexpr int BLK = FPB * kFragBytes;
+    const int nseg = a.job_nseg[j];
 
-    // input block kb -> (segment, block in segment)
-    int in_seg[4], in_blk[4];
-    bool kval[4], nval[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int kb = 4 * kbg + q;
-        kval[q] = kb < KB;
-        const int s = (a.job_nin[j] > 1 && kb >= a.job_in_blocks[j][0]) ? 1 : 0;
-        in_seg[q] = s;
-        in_blk[q] = kb - (s ? a.job_in_blocks[j][0] : 0);
-        nval[q] = 4 * nbg + q < NB;
-    }
-    const bool do_bias = kbg == 0;
+    // stage tile t into buffer b (the job's blocks, dz segments first)
+    auto stage = [&](int64_t t, int b) {
+        char* dst = lds + b * a.stage_bytes;
+        int blk0 = 0;
+        for (int s = 0; s < nseg; ++s) {
+            const int nb = a.seg_blocks[j][s];
+            const char* src = (a.seg_isws[j][s] ? a.ws : a.saved) + a.seg_off[j][s] + t * nb * BLK;
+            const int pieces = nb * FPB;  // 1-KB wave pieces
+            for (int pc = wv; pc < pieces; pc += kWaves)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(src + pc * kFragBytes + lane * 16),
+                    (__attribute__((address_space(3))) void*)(dst + (blk0 * FPB + pc) * kFragBytes), 16, 0, 0);
+            blk0 += nb;
+        }
+    };
 
     f32x16 acc[4][4];
 #pragma unroll
@@ -612,54 +844,79 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void mlp_dw_kernel(DwArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) zero(acc[p][q]);
     float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    bool nval[4], kval[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        nval[q] = active && 4 * nbg + q < NBz;
+        kval[q] = active && 4 * kbg + q < KB;
+    }
+    const bool do_bias = active && kbg == 0;
 
-    const char* dz = a.ws + a.job_dz_off[j];
+    if (t0 < t1) stage(t0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     for (int64_t t = t0; t < t1; ++t) {
-        bf16x8 ab[4][2], bb[4][2];
-        f32x4 af[4][4], bf[4][4];
+        const int cur = static_cast<int>((t - t0) & 1);
+        if (t + 1 < t1) stage(t + 1, cur ^ 1);
+        const char* buf = lds + cur * a.stage_bytes;
+        if (active) {
+            if constexpr (PREC == NR_PREC_BF16) {
 #pragma unroll
-        for (int p = 0; p < 4; ++p)
-            if (nval[p]) load_rowfrag<PREC>(dz, t, a.job_dz_F[j], 32 * (4 * nbg + p), lane, ab[p], af[p]);
+                for (int ks = 0; ks < 2; ++ks) {
+                    bf16x8 A[4], Bm[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (kval[q])
-                load_rowfrag<PREC>(a.saved + a.job_in_off[j][in_seg[q]], t, a.job_in_F[j][in_seg[q]], 32 * in_blk[q],
-                                   lane, bb[q], bf[q]);
+                    for (int p = 0; p < 4; ++p)
+                        if (nval[p]) A[p] = dw_frag_bf16(buf + (4 * nbg + p) * BLK, ks, lane);
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            if (!nval[p]) continue;
-            if (do_bias) {
-                if constexpr (PREC == NR_PREC_BF16) {
+                    for (int q = 0; q < 4; ++q)
+                        if (kval[q]) Bm[q] = dw_frag_bf16(buf + (NBz + 4 * kbg + q) * BLK, ks, lane);
 #pragma unroll
-                    for (int s = 0; s < 2; ++s)
+                    for (int p = 0; p < 4; ++p) {
+                        if (!nval[p]) continue;
+                        if (do_bias)
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) bsum[p] += static_cast<float>(ab[p][s][e]);
-                } else {
+                            for (int e = 0; e < 8; ++e) bsum[p] += static_cast<float>(A[p][e]);
 #pragma unroll
-                    for (int s = 0; s < 4; ++s)
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) bsum[p] += af[p][s][e];
+                        for (int q = 0; q < 4; ++q)
+                            if (kval[q]) acc[p][q] = mfma_bf16(A[p], Bm[q], acc[p][q]);
+                    }
                 }
-            }
+            } else {
+                // fp32 image [tq][L][4]: operand row r <-> (hh = r>>4, reg i = r&15 -> frag i>>2, elem i&3)
+                const int r = lane & 31, kk = lane >> 5;
+                const int hh = r >> 4, i = r & 15;
+                const int off = ((i >> 2) * 64 + 32 * hh) * 16 + (i & 3) * 4;
+#pragma unroll 4
+                for (int ss = 0; ss < 16; ++ss) {
+                    const int m = 2 * ss + kk;
+                    float A[4], Bv[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (!kval[q]) continue;
-                if constexpr (PREC == NR_PREC_BF16) {
-                    acc[p][q] = mfma_bf16(ab[p][0], bb[q][0], acc[p][q]);
-                    acc[p][q] = mfma_bf16(ab[p][1], bb[q][1], acc[p][q]);
-                } else {
+                    for (int p = 0; p < 4; ++p)
+                        A[p] = nval[p] ? *reinterpret_cast<const float*>(buf + (4 * nbg + p) * BLK + off + m * 16)
+                                       : 0.f;
 #pragma unroll
-                    for (int s = 0; s < 4; ++s)
+                    for (int q = 0; q < 4; ++q)
+                        Bv[q] = kval[q] ? *reinterpret_cast<const float*>(buf + (NBz + 4 * kbg + q) * BLK + off +
+                                                                          m * 16)
+                                        : 0.f;
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) acc[p][q] = mfma_f32(af[p][s][e], bf[q][s][e], acc[p][q]);
+                    for (int p = 0; p < 4; ++p) {
+                        if (!nval[p]) continue;
+                        if (do_bias) bsum[p] += A[p];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (kval[q]) acc[p][q] = mfma_f32(A[p], Bv[q], acc[p][q]);
+                    }
                 }
             }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
     }
-    // write the slab: row = dz row n, col = input feature k (padded)
+    if (!active) return;
     float* slab = a.slabs + static_cast<int64_t>(chunk) * a.slab_floats_per_chunk + a.job_slab[j];
     const int ld = KB * 32 + 1;
-    const int h = lane >> 5, ml = lane & 31;
+    const int hl = lane >> 5, ml = lane & 31;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         if (!nval[p]) continue;
@@ -668,70 +925,67 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void mlp_dw_kernel(DwArgs a) {
             if (!kval[q]) continue;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = 32 * (4 * nbg + p) + acc_row(r, h);
-                const int col = 32 * (4 * kbg + q) + ml;
+                const int row = 32 * (4 * nbg + p) + dw_feat(acc_row(r, hl));
+                const int col = 32 * (4 * kbg + q) + dw_feat(ml);
                 slab[static_cast<int64_t>(row) * ld + col] = acc[p][q][r];
             }
         }
         if (do_bias) {
             const float tot = bsum[p] + __shfl_xor(bsum[p], 32);
-            if (h == 0) slab[static_cast<int64_t>(32 * (4 * nbg + p) + ml) * ld + KB * 32] = tot;
+            if (hl == 0) slab[static_cast<int64_t>(32 * (4 * nbg + p) + dw_feat(ml)) * ld + KB * 32] = tot;
         }
     }
 }
 
-// g_params[param] = sum over chunks of the slab entry it maps to (chunk order:
-// deterministic).  One thread per parameter.
+// g_params[param] = sum over chunks of its slab entry (fixed chunk order: deterministic).
 struct ReduceArgs {
     const float* slabs;
     float* g;
     int64_t param_count;
     int chunks;
     int64_t slab_floats_per_chunk;
-    int n_jobs;
-    int64_t job_p0[kMaxJobs + 1];  // first flat parameter of each job (weights then bias)
-    int64_t job_w_off[kMaxJobs], job_b_off[kMaxJobs];
-    int job_rows[kMaxJobs], job_in[kMaxJobs], job_KB[kMaxJobs], job_row0[kMaxJobs];
-    int job_nseg[kMaxJobs];
-    int job_seg_col0[kMaxJobs][kMaxSeg], job_seg_w[kMaxJobs][kMaxSeg], job_seg_blk0[kMaxJobs][kMaxSeg];
-    int64_t job_slab[kMaxJobs];
+    int n_red;
+    int red_row0[kMaxJobs + 2], red_rows[kMaxJobs + 2], red_in[kMaxJobs + 2], red_KB[kMaxJobs + 2];
+    int64_t red_w_off[kMaxJobs + 2], red_b_off[kMaxJobs + 2], red_slab[kMaxJobs + 2];
+    int red_nseg[kMaxJobs + 2];
+    int red_seg_col0[kMaxJobs + 2][kMaxSeg], red_seg_w[kMaxJobs + 2][kMaxSeg], red_seg_blk0[kMaxJobs + 2][kMaxSeg];
 };
 
 __global__ void mlp_dw_reduce_kernel(ReduceArgs a) {
     const int64_t pidx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (pidx >= a.param_count) return;
-    // find the job whose weight or bias range holds pidx
-    int j = -1;
-    int64_t row = 0, col = -1;  // col = -1 => bias
-    for (int q = 0; q < a.n_jobs; ++q) {
-        const int64_t wsz = static_cast<int64_t>(a.job_rows[q]) * a.job_in[q];
-        if (pidx >= a.job_w_off[q] && pidx < a.job_w_off[q] + wsz) {
-            j = q;
-            const int64_t e = pidx - a.job_w_off[q];
-            row = e / a.job_in[q];
-            const int c = static_cast<int>(e % a.job_in[q]);
-            // W column c -> padded slab column
-            for (int s = 0; s < a.job_nseg[q]; ++s)
-                if (c >= a.job_seg_col0[q][s] && c < a.job_seg_col0[q][s] + a.job_seg_w[q][s])
-                    col = 32 * a.job_seg_blk0[q][s] + (c - a.job_seg_col0[q][s]);
+    int q = -1;
+    int64_t row = 0, col = -1;
+    for (int k = 0; k < a.n_red; ++k) {
+        const int64_t wsz = static_cast<int64_t>(a.red_rows[k]) * a.red_in[k];
+        if (pidx >= a.red_w_off[k] && pidx < a.red_w_off[k] + wsz) {
+            q = k;
+            const int64_t e = pidx - a.red_w_off[k];
+            row = e / a.red_in[k];
+            const int c = static_cast<int>(e % a.red_in[k]);
+            for (int s = 0; s < a.red_nseg[k]; ++s)
+                if (c >= a.red_seg_col0[k][s] && c < a.red_seg_col0[k][s] + a.red_seg_w[k][s])
+                    col = 32 * a.red_seg_blk0[k][s] + (c - a.red_seg_col0[k][s]);
             break;
         }
-        if (pidx >= a.job_b_off[q] && pidx < a.job_b_off[q] + a.job_rows[q]) {
-            j = q;
-            row = pidx - a.job_b_off[q];
-            col = static_cast<int64_t>(a.job_KB[q]) * 32;
+        if (pidx >= a.red_b_off[k] && pidx < a.red_b_off[k] + a.red_rows[k]) {
+            q = k;
+            row = pidx - a.red_b_off[k];
+            col = static_cast<int64_t>(a.red_KB[k]) * 32;
             break;
         }
     }
-    if (j < 0) return;
-    const int ld = a.job_KB[j] * 32 + 1;
-    const float* s = a.slabs + a.job_slab[j] + (row + a.job_row0[j]) * ld + col;
+    if (q < 0 || col < 0) return;
+    const int64_t ld = static_cast<int64_t>(a.red_KB[q]) * 32 + 1;
+    const float* s = a.slabs + a.red_slab[q] + (row + a.red_row0[q]) * ld + col;
     float acc = 0.f;
     for (int c = 0; c < a.chunks; ++c) acc += s[static_cast<int64_t>(c) * a.slab_floats_per_chunk];
     a.g[pidx] = acc;
 }
 
 // ---------------------------------------------------------------- pack ----
+// Image element e of layer l (fwd: W, bwd: W^T), chunk-major:
+//   e = (((kblock * ROWBLOCKS + rowblock) * FPB + frag) * 64 + lane) * EPL + el
 struct PackArgs {
     const float* params;
     char* packed;
@@ -740,10 +994,11 @@ struct PackArgs {
     int64_t w_off[kMaxMfmaLayers];
     int in[kMaxMfmaLayers], NB[kMaxMfmaLayers], KB[kMaxMfmaLayers], nseg[kMaxMfmaLayers];
     int seg_col0[kMaxMfmaLayers][kMaxSeg], seg_w[kMaxMfmaLayers][kMaxSeg], seg_blk[kMaxMfmaLayers][kMaxSeg];
-    int64_t pk[kMaxMfmaLayers];   // byte offset of the fwd image; bwd image follows
-    int64_t cum[kMaxMfmaLayers + 1];  // cumulative element counts (fwd+bwd per layer)
+    int64_t pk[kMaxMfmaLayers], pkb[kMaxMfmaLayers];
+    int64_t cum[kMaxMfmaLayers + 1];
 };
 
+// W column of local input index c (0..31) in input block kb, or -1 for padding.
 __device__ __forceinline__ int pack_col(const PackArgs& a, int l, int kb, int c) {
     int blk0 = 0;
     for (int s = 0; s < a.nseg[l]; ++s) {
@@ -775,21 +1030,42 @@ __global__ void mlp_pack_kernel(PackArgs a) {
     const int h = lane >> 5, i = lane & 31;
     const int kk = bf ? 16 * sub + 8 * (el >> 2) + 4 * h + (el & 3) : acc_row(4 * sub + el, h);
     int row, col;
-    if (!bwd) {  // W fragment (nb, kb): A[i][k] = W[32nb+i][col(kb,k)]
-        const int nb = static_cast<int>(blk / a.KB[l]), kb = static_cast<int>(blk % a.KB[l]);
+    if (!bwd) {  // W: A[i][k] = W[32nb + i][col(kb, k)], chunk kb, row block nb
+        const int kb = static_cast<int>(blk / a.NB[l]), nb = static_cast<int>(blk % a.NB[l]);
         row = 32 * nb + i;
         col = pack_col(a, l, kb, kk);
-    } else {  // W^T fragment (ib, ob): A[i][k] = W[32ob+k][col(ib,i)]
-        const int ib = static_cast<int>(blk / a.NB[l]), ob = static_cast<int>(blk % a.NB[l]);
+    } else {  // W^T: A[i][k] = W[32ob + k][col(ib, i)], chunk ob, row block ib
+        const int ob = static_cast<int>(blk / a.KB[l]), ib = static_cast<int>(blk % a.KB[l]);
         row = 32 * ob + kk;
         col = pack_col(a, l, ib, i);
     }
     const float v = col >= 0 ? a.params[a.w_off[l] + static_cast<int64_t>(row) * a.in[l] + col] : 0.f;
-    char* dst = a.packed + a.pk[l] + (bwd ? img * (bf ? 2 : 4) : 0);
+    char* dst = a.packed + (bwd ? a.pkb[l] : a.pk[l]);
     if (bf)
         reinterpret_cast<unsigned short*>(dst)[e] = bf16_bits(v);
     else
         reinterpret_cast<float*>(dst)[e] = v;
+}
+
+// Vector images: element idx of a vector of NB blocks <-> feature 32*(idx>>5) + acc_row(idx&15, (idx>>4)&1).
+struct PackVecArgs {
+    const float* params;
+    char* packed;
+    int nv;                                   // vectors: n_lin biases, w_sigma, 3 rows of W_rgb
+    int64_t src[kMaxMfmaLayers + 4];          // float offset in params
+    int len[kMaxMfmaLayers + 4];              // valid features
+    int64_t dst[kMaxMfmaLayers + 4];          // byte offset in packed
+    int cum[kMaxMfmaLayers + 5];              // image elements (NB*32) prefix
+};
+
+__global__ void mlp_pack_vec_kernel(PackVecArgs a) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.cum[a.nv]) return;
+    int v = 0;
+    while (g >= a.cum[v + 1]) ++v;
+    const int idx = g - a.cum[v];
+    const int f = 32 * (idx >> 5) + acc_row(idx & 15, (idx >> 4) & 1);
+    reinterpret_cast<float*>(a.packed + a.dst[v])[idx] = f < a.len[v] ? a.params[a.src[v] + f] : 0.f;
 }
 
 }  // namespace nr
@@ -807,35 +1083,85 @@ bool plan_or_error(const NrMlpConfig* cfg, MlpPlan* p) {
     return true;
 }
 
+// Workgroup shape of the bf16 forward / backward kernels: NT threads, one
+// 32-sample tile per wave, all waves sharing one LDS weight stream.  256 = 4
+// waves with the full 512-register budget (1 wave per SIMD); 512 = 8 waves at
+// 256 registers (2 waves per SIMD).  Measured on MI355X at M = 786,432 (r01):
+// forward (training) 3.25 ms at 256 vs 4.09 ms at 512 (the 512 build spills);
+// backward dX 2.12 ms at 256 vs 1.70 ms at 512.
+#ifndef NR_FWD_NT
+#define NR_FWD_NT 256
+#endif
+#ifndef NR_BWD_NT
+#define NR_BWD_NT 512
+#endif
+#define NR_FWD_TPW 1
+
+void add_stream_layer(StreamDesc& sd, int nchunks, int chunk_kb) {
+    for (int c = 0; c < nchunks && sd.nq < kMaxChunks; ++c) sd.ckb[sd.nq++] = chunk_kb;
+}
+
+int max_chunk(const StreamDesc& sd) {
+    int m = 0;
+    for (int q = 0; q < sd.nq; ++q) m = sd.ckb[q] * 1024 > m ? sd.ckb[q] * 1024 : m;
+    return m;
+}
+
 template <int PREC, bool TRAIN>
-int launch_fwd(const MlpPlan& p, const FwdArgs& a, hipStream_t s) {
-    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, kWavesPerBlock))), block(64 * kWavesPerBlock);
-#define NR_FWD(XB_, DB_)                                                                         \
-    if (p.XB == XB_ && p.DB == DB_) {                                                            \
-        hipLaunchKernelGGL((mlp_fwd_kernel<PREC, XB_, DB_, TRAIN>), grid, block, 0, s, a);       \
-        return check_launch("nr_mlp_forward");                                                   \
+int launch_fwd(const MlpPlan& p, FwdArgs& a, hipStream_t s) {
+    constexpr int TPW = NR_FWD_TPW, NT = PREC == NR_PREC_BF16 ? NR_FWD_NT : 256;
+    constexpr int G = (PREC == NR_PREC_BF16 ? 16384 : 32768) / (NT * 16);  // one 16 / 32 KB chunk
+    const int mc = max_chunk(a.sd);
+    if (mc > G * NT * 16) {
+        set_error("nr_mlp_forward: chunk of %d bytes exceeds the stager", mc);
+        return NR_EARG;
+    }
+    a.slot_bytes = mc;
+    const size_t lds = 2 * static_cast<size_t>(mc);
+    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, (NT / 64) * TPW))), block(NT);
+#define NR_FWD(XB_, DB_)                                                                                 \
+    if (p.XB == XB_ && p.DB == DB_) {                                                                    \
+        hipLaunchKernelGGL((mlp_fwd_kernel<PREC, XB_, DB_, TRAIN, TPW, G, NT>), grid, block, lds, s, a); \
+        return check_launch("nr_mlp_forward");                                                           \
     }
     NR_FWD(2, 1)
+#ifndef NR_MLP_DEV  // dev builds (register/ISA inspection) compile the default model only
     NR_FWD(2, 0)
     NR_FWD(1, 1)
+    NR_FWD(1, 0)
+#endif
 #undef NR_FWD
-    set_error("nr_mlp_forward: no kernel instance for XB=%d DB=%d (pos_freqs/dir_freqs)", p.XB, p.DB);
+    set_error("nr_mlp_forward: no kernel instance for XB=%d DB=%d", p.XB, p.DB);
     return NR_EARG;
 }
 
-template <int PREC>
-int launch_bwd(const MlpPlan& p, const BwdArgs& a, hipStream_t s) {
-    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, kWavesPerBlock))), block(64 * kWavesPerBlock);
-#define NR_BWD(XB_, DB_)                                                                   \
-    if (p.XB == XB_ && p.DB == DB_) {                                                      \
-        hipLaunchKernelGGL((mlp_bwd_kernel<PREC, XB_, DB_>), grid, block, 0, s, a);        \
-        return check_launch("nr_mlp_backward");                                            \
+template <int PREC, bool WX>
+int launch_bwd(const MlpPlan& p, BwdArgs& a, hipStream_t s) {
+    // the input-gradient variant also carries d x_enc through the trunk: 4 waves, 512 registers
+    constexpr int TPW = 1, NT = (WX || PREC != NR_PREC_BF16) ? 256 : NR_BWD_NT;
+    // one chunk of the skip layer's W^T: (XB + 8) blocks, at most 20 / 40 KB
+    constexpr int G = ((PREC == NR_PREC_BF16 ? 20480 : 40960) + NT * 16 - 1) / (NT * 16);
+    const int mc = max_chunk(a.sd);
+    if (mc > G * NT * 16) {
+        set_error("nr_mlp_backward_dx: chunk of %d bytes exceeds the stager", mc);
+        return NR_EARG;
+    }
+    a.slot_bytes = mc;
+    const size_t lds = 2 * static_cast<size_t>(mc);
+    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, (NT / 64) * TPW))), block(NT);
+#define NR_BWD(XB_, DB_)                                                                              \
+    if (p.XB == XB_ && p.DB == DB_) {                                                                 \
+        hipLaunchKernelGGL((mlp_bwd_kernel<PREC, XB_, DB_, TPW, G, NT, WX>), grid, block, lds, s, a); \
+        return check_launch("nr_mlp_backward_dx");                                                    \
     }
     NR_BWD(2, 1)
+#ifndef NR_MLP_DEV  // dev builds (register/ISA inspection) compile the default model only
     NR_BWD(2, 0)
     NR_BWD(1, 1)
+    NR_BWD(1, 0)
+#endif
 #undef NR_BWD
-    set_error("nr_mlp_backward: no kernel instance for XB=%d DB=%d (pos_freqs/dir_freqs)", p.XB, p.DB);
+    set_error("nr_mlp_backward_dx: no kernel instance for XB=%d DB=%d", p.XB, p.DB);
     return NR_EARG;
 }
 
@@ -890,12 +1216,29 @@ int nr_mlp_pack(const NrMlpConfig* cfg, const float* params, void* packed, nr_st
             a.seg_blk[l][s] = d.seg[s].blocks;
         }
         a.pk[l] = d.pk_fwd;
+        a.pkb[l] = d.pk_bwd;
         const int64_t elems = static_cast<int64_t>(d.NB) * d.KB * 1024;  // 32x32 elements per block
         a.cum[l + 1] = a.cum[l] + 2 * elems;
     }
     const int64_t total = a.cum[p.n_lin];
-    hipLaunchKernelGGL(mlp_pack_kernel, dim3(static_cast<unsigned>(ceil_div_ll(total, 256))), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), a);
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(mlp_pack_kernel, dim3(static_cast<unsigned>(ceil_div_ll(total, 256))), dim3(256), 0, s, a);
+    NR_LAUNCH_CHECK("nr_mlp_pack");
+    PackVecArgs v;
+    std::memset(&v, 0, sizeof(v));
+    v.params = params;
+    v.packed = static_cast<char*>(packed);
+    auto add_vec = [&](int64_t src, int len, int64_t dst, int nblk) {
+        v.src[v.nv] = src;
+        v.len[v.nv] = len;
+        v.dst[v.nv] = dst;
+        v.cum[v.nv + 1] = v.cum[v.nv] + nblk * 32;
+        v.nv++;
+    };
+    for (int l = 0; l < p.n_lin; ++l) add_vec(p.lin[l].b_off, p.lin[l].out, p.lin[l].vb, p.lin[l].NB);
+    add_vec(p.sig_w, kHidden, p.vsig, kHB);
+    for (int c = 0; c < 3; ++c) add_vec(p.rgb_w + c * (kHidden / 2), kHidden / 2, p.vrgb + c * (kHidden / 2) * 4, kHB / 2);
+    hipLaunchKernelGGL(mlp_pack_vec_kernel, dim3(ceil_div(v.cum[v.nv], 256)), dim3(256), 0, s, v);
     NR_LAUNCH_CHECK("nr_mlp_pack");
     return NR_OK;
 }
@@ -907,6 +1250,7 @@ int nr_mlp_forward(const NrMlpConfig* cfg, const void* packed, const float* para
     NR_REQUIRE(packed && params && x && rgb && sigma && M >= 0, "nr_mlp_forward: null pointer");
     NR_REQUIRE(!p.use_vd || d, "nr_mlp_forward: use_view_dirs needs d (model.py:187-191)");
     NR_REQUIRE((reinterpret_cast<uintptr_t>(saved) & 15) == 0, "nr_mlp_forward: saved must be 16-byte aligned");
+    NR_REQUIRE((reinterpret_cast<uintptr_t>(packed) & 15) == 0, "nr_mlp_forward: packed must be 16-byte aligned");
     if (M == 0) return NR_OK;
     const MlpSizes z = make_sizes(p, M);
     FwdArgs a;
@@ -924,19 +1268,17 @@ int nr_mlp_forward(const NrMlpConfig* cfg, const void* packed, const float* para
     a.Ld = p.Ld;
     a.n_layers = p.n_layers;
     a.skips = p.skips;
+    a.sd.base = p.lin[0].pk_fwd;
     for (int l = 0; l < p.n_lin; ++l) {
-        a.pk[l] = p.lin[l].pk_fwd;
-        a.KB[l] = p.lin[l].KB;
-        a.bias[l] = p.lin[l].b_off;
+        const LinearDesc& dl = p.lin[l];
+        add_stream_layer(a.sd, dl.KB, dl.NB * p.fpb);
+        a.vb[l] = dl.vb;
     }
-    a.sig_w = p.sig_w;
+    a.vsig = p.vsig;
+    a.vrgb = p.vrgb;
     a.sig_b = p.sig_b;
-    a.rgb_w = p.rgb_w;
     a.rgb_b = p.rgb_b;
-    for (int t = 0; t < p.n_saved; ++t) {
-        a.sv_off[t] = z.saved_off[t];
-        a.sv_F[t] = p.sv_F[t];
-    }
+    for (int t = 0; t < p.n_saved; ++t) a.sv_off[t] = z.saved_off[t];
     a.sv_feat = p.sv_feat;
     a.sv_denc = p.sv_denc;
     a.sv_hc = p.sv_hc;
@@ -948,23 +1290,20 @@ int nr_mlp_forward(const NrMlpConfig* cfg, const void* packed, const float* para
     return saved ? launch_fwd<NR_PREC_FP32, true>(p, a, s) : launch_fwd<NR_PREC_FP32, false>(p, a, s);
 }
 
-int nr_mlp_backward(const NrMlpConfig* cfg, const void* packed, const float* params, const float* x, const float* d,
-                    int64_t M, const float* rgb, const float* sigma, const void* saved, const float* g_rgb,
-                    const float* g_sigma, float* g_params, float* g_x, float* g_d, void* workspace,
-                    nr_stream_t stream) {
+int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* params, const float* x,
+                       const float* d, int64_t M, const float* rgb, const float* sigma, const void* saved,
+                       const float* g_rgb, const float* g_sigma, float* g_x, float* g_d, void* workspace,
+                       nr_stream_t stream) {
     MlpPlan p;
     if (!plan_or_error(cfg, &p)) return NR_EARG;
-    NR_REQUIRE(packed && params && x && rgb && sigma && saved && g_rgb && g_sigma && g_params && workspace && M >= 0,
-               "nr_mlp_backward: null pointer");
-    NR_REQUIRE(!g_d || (d && p.use_vd), "nr_mlp_backward: g_d needs d and use_view_dirs");
+    NR_REQUIRE(packed && params && x && rgb && sigma && saved && g_rgb && g_sigma && workspace && M >= 0,
+               "nr_mlp_backward_dx: null pointer");
+    NR_REQUIRE(!g_d || (d && p.use_vd), "nr_mlp_backward_dx: g_d needs d and use_view_dirs");
+    NR_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0,
+               "nr_mlp_backward_dx: workspace must be 16-byte aligned");
+    if (M == 0) return NR_OK;
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    if (M == 0) {
-        hipMemsetAsync(g_params, 0, sizeof(float) * p.param_count, s);
-        return check_launch("nr_mlp_backward");
-    }
     const MlpSizes z = make_sizes(p, M);
-    char* ws = static_cast<char*>(workspace);
-
     BwdArgs b;
     std::memset(&b, 0, sizeof(b));
     b.packed = static_cast<const char*>(packed);
@@ -978,115 +1317,140 @@ int nr_mlp_backward(const NrMlpConfig* cfg, const void* packed, const float* par
     b.g_x = g_x;
     b.g_d = g_d;
     b.saved = static_cast<const char*>(saved);
-    b.ws = ws;
+    b.ws = static_cast<char*>(workspace);
     b.M = M;
     b.tiles = z.tiles;
     b.L = p.L;
     b.Ld = p.Ld;
     b.n_layers = p.n_layers;
     b.skips = p.skips;
-    for (int l = 0; l < p.n_lin; ++l) {
-        b.pkT[l] = p.lin[l].pk_bwd;
-        b.NB[l] = p.lin[l].NB;
-    }
-    b.sig_w = p.sig_w;
-    b.rgb_w = p.rgb_w;
+    const int n = p.n_layers;
+    const bool wx = g_x != nullptr || g_d != nullptr;
+    auto add_T = [&](int l) { add_stream_layer(b.sd, p.lin[l].NB, p.lin[l].KB * p.fpb); };
+    b.sd.base = p.lin[n + 1].pk_bwd;
+    add_T(n + 1);  // dir^T
+    add_T(n);      // feat^T
+    for (int i = n - 1; i >= 1; --i) add_T(i);
+    if (wx) add_T(0);
+    b.vsig = p.vsig;
+    b.vrgb = p.vrgb;
     b.mask_off = z.mask_off;
     b.n_mask = p.n_mask;
     for (int t = 0; t < p.n_ws; ++t) b.ws_off[t] = z.ws_off[t];
     b.ws_feat = p.ws_feat;
     b.ws_dir = p.ws_dir;
     b.ws_heads = p.ws_heads;
-    int rc = p.prec == NR_PREC_BF16 ? launch_bwd<NR_PREC_BF16>(p, b, s) : launch_bwd<NR_PREC_FP32>(p, b, s);
-    if (rc) return rc;
+    if (p.prec == NR_PREC_BF16)
+        return wx ? launch_bwd<NR_PREC_BF16, true>(p, b, s) : launch_bwd<NR_PREC_BF16, false>(p, b, s);
+    return wx ? launch_bwd<NR_PREC_FP32, true>(p, b, s) : launch_bwd<NR_PREC_FP32, false>(p, b, s);
+}
 
-    // dW over all jobs, split into z.chunks sample chunks
+int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, void* workspace, nr_stream_t stream) {
+    MlpPlan p;
+    if (!plan_or_error(cfg, &p)) return NR_EARG;
+    NR_REQUIRE(saved && workspace && M >= 0, "nr_mlp_backward_dw: null pointer");
+    if (M == 0) return NR_OK;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const MlpSizes z = make_sizes(p, M);
+    char* ws = static_cast<char*>(workspace);
     DwArgs w;
     std::memset(&w, 0, sizeof(w));
     w.saved = static_cast<const char*>(saved);
     w.ws = ws;
     w.slabs = reinterpret_cast<float*>(ws + z.slab_off);
     w.tiles = z.tiles;
-    w.chunks = z.chunks;
     w.tiles_per_chunk = static_cast<int>(ceil_div_ll(z.tiles, z.chunks));
     w.n_jobs = p.n_jobs;
     w.slab_floats_per_chunk = p.slab_floats_per_chunk;
-    int wg = 0;
+    int wg = 0, max_blk = 0;
     for (int j = 0; j < p.n_jobs; ++j) {
         const DwJob& jb = p.job[j];
         w.job_wg0[j] = wg;
-        w.job_nbg[j] = (jb.NB + 3) / 4;
+        w.job_nbg[j] = (jb.NBz + 3) / 4;
         w.job_sg[j] = w.job_nbg[j] * ((jb.KB + 3) / 4);
-        wg += z.chunks * ((w.job_sg[j] + kWavesPerBlock - 1) / kWavesPerBlock);
-        w.job_NB[j] = jb.NB;
+        w.job_groups[j] = (w.job_sg[j] + kWaves - 1) / kWaves;
+        wg += z.chunks * w.job_groups[j];
+        w.job_NBz[j] = jb.NBz;
         w.job_KB[j] = jb.KB;
-        w.job_row0[j] = jb.dz_row0;
-        w.job_nin[j] = jb.nin;
-        w.job_dz_off[j] = z.ws_off[jb.dz_tensor];
-        w.job_dz_F[j] = p.ws_F[jb.dz_tensor];
-        for (int q = 0; q < jb.nin; ++q) {
-            w.job_in_off[j][q] = z.saved_off[jb.in_tensor[q]];
-            w.job_in_F[j][q] = p.sv_F[jb.in_tensor[q]];
-            w.job_in_blocks[j][q] = jb.in_blocks[q];
+        int ns = 0;
+        for (int q = 0; q < jb.ndz; ++q, ++ns) {
+            w.seg_off[j][ns] = (jb.dz[q].is_ws ? z.ws_off : z.saved_off)[jb.dz[q].tensor];
+            w.seg_blocks[j][ns] = jb.dz[q].blocks;
+            w.seg_isws[j][ns] = jb.dz[q].is_ws;
         }
+        for (int q = 0; q < jb.nin; ++q, ++ns) {
+            w.seg_off[j][ns] = (jb.in[q].is_ws ? z.ws_off : z.saved_off)[jb.in[q].tensor];
+            w.seg_blocks[j][ns] = jb.in[q].blocks;
+            w.seg_isws[j][ns] = jb.in[q].is_ws;
+        }
+        w.job_nseg[j] = ns;
         w.job_slab[j] = jb.slab_off;
+        max_blk = jb.NBz + jb.KB > max_blk ? jb.NBz + jb.KB : max_blk;
     }
     w.job_wg0[p.n_jobs] = wg;
+    w.stage_bytes = max_blk * p.fpb * kFragBytes;
+    const size_t lds = 2 * static_cast<size_t>(w.stage_bytes);
+    NR_REQUIRE(lds <= 160 * 1024, "nr_mlp_backward_dw: %zu bytes of LDS staging exceeds 160 KiB", lds);
     if (p.prec == NR_PREC_BF16)
-        hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_BF16>, dim3(wg), dim3(64 * kWavesPerBlock), 0, s, w);
+        hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_BF16>, dim3(wg), dim3(kThreads), lds, s, w);
     else
-        hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_FP32>, dim3(wg), dim3(64 * kWavesPerBlock), 0, s, w);
-    NR_LAUNCH_CHECK("nr_mlp_backward (dW)");
+        hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_FP32>, dim3(wg), dim3(kThreads), lds, s, w);
+    NR_LAUNCH_CHECK("nr_mlp_backward_dw");
+    return NR_OK;
+}
 
+int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M, const void* workspace, float* g_params,
+                           nr_stream_t stream) {
+    MlpPlan p;
+    if (!plan_or_error(cfg, &p)) return NR_EARG;
+    NR_REQUIRE(workspace && g_params && M >= 0, "nr_mlp_backward_reduce: null pointer");
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    if (M == 0) {
+        (void)hipMemsetAsync(g_params, 0, sizeof(float) * p.param_count, s);
+        return check_launch("nr_mlp_backward_reduce");
+    }
+    const MlpSizes z = make_sizes(p, M);
     ReduceArgs r;
     std::memset(&r, 0, sizeof(r));
-    r.slabs = w.slabs;
+    r.slabs = reinterpret_cast<const float*>(static_cast<const char*>(workspace) + z.slab_off);
     r.g = g_params;
     r.param_count = p.param_count;
     r.chunks = z.chunks;
     r.slab_floats_per_chunk = p.slab_floats_per_chunk;
-    r.n_jobs = p.n_jobs;
-    for (int j = 0; j < p.n_jobs; ++j) {
-        const DwJob& jb = p.job[j];
-        if (jb.layer >= 0) {
-            const LinearDesc& ld = p.lin[jb.layer];
-            r.job_w_off[j] = ld.w_off;
-            r.job_b_off[j] = ld.b_off;
-            r.job_in[j] = ld.in;
-            r.job_nseg[j] = ld.nseg;
-            int blk = 0;
-            for (int q = 0; q < ld.nseg; ++q) {
-                r.job_seg_col0[j][q] = ld.seg[q].col0;
-                r.job_seg_w[j][q] = ld.seg[q].width;
-                r.job_seg_blk0[j][q] = blk;
-                blk += ld.seg[q].blocks;
-            }
-        } else if (jb.layer == -1) {  // sigma head: W (1, hidden)
-            r.job_w_off[j] = p.sig_w;
-            r.job_b_off[j] = p.sig_b;
-            r.job_in[j] = kHidden;
-            r.job_nseg[j] = 1;
-            r.job_seg_col0[j][0] = 0;
-            r.job_seg_w[j][0] = kHidden;
-            r.job_seg_blk0[j][0] = 0;
-        } else {  // rgb head: W (3, hidden/2)
-            r.job_w_off[j] = p.rgb_w;
-            r.job_b_off[j] = p.rgb_b;
-            r.job_in[j] = kHidden / 2;
-            r.job_nseg[j] = 1;
-            r.job_seg_col0[j][0] = 0;
-            r.job_seg_w[j][0] = kHidden / 2;
-            r.job_seg_blk0[j][0] = 0;
+    r.n_red = p.n_red;
+    for (int k = 0; k < p.n_red; ++k) {
+        const ReduceRange& rr = p.red[k];
+        r.red_row0[k] = rr.row0;
+        r.red_rows[k] = rr.rows;
+        r.red_in[k] = rr.in;
+        r.red_KB[k] = p.job[rr.job].KB;
+        r.red_w_off[k] = rr.w_off;
+        r.red_b_off[k] = rr.b_off;
+        r.red_slab[k] = p.job[rr.job].slab_off;
+        r.red_nseg[k] = rr.nseg;
+        for (int q = 0; q < rr.nseg; ++q) {
+            r.red_seg_col0[k][q] = rr.seg_col0[q];
+            r.red_seg_w[k][q] = rr.seg_w[q];
+            r.red_seg_blk0[k][q] = rr.seg_blk0[q];
         }
-        r.job_rows[j] = jb.rows;
-        r.job_KB[j] = jb.KB;
-        r.job_row0[j] = jb.dz_row0;
-        r.job_slab[j] = jb.slab_off;
     }
     hipLaunchKernelGGL(mlp_dw_reduce_kernel, dim3(static_cast<unsigned>(ceil_div_ll(p.param_count, 256))), dim3(256),
                        0, s, r);
-    NR_LAUNCH_CHECK("nr_mlp_backward (dW reduce)");
+    NR_LAUNCH_CHECK("nr_mlp_backward_reduce");
     return NR_OK;
+}
+
+int nr_mlp_backward(const NrMlpConfig* cfg, const void* packed, const float* params, const float* x, const float* d,
+                    int64_t M, const float* rgb, const float* sigma, const void* saved, const float* g_rgb,
+                    const float* g_sigma, float* g_params, float* g_x, float* g_d, void* workspace,
+                    nr_stream_t stream) {
+    NR_REQUIRE(g_params, "nr_mlp_backward: null g_params");
+    int rc = nr_mlp_backward_dx(cfg, packed, params, x, d, M, rgb, sigma, saved, g_rgb, g_sigma, g_x, g_d, workspace,
+                                stream);
+    if (rc) return rc;
+    rc = nr_mlp_backward_dw(cfg, M, saved, workspace, stream);
+    if (rc) return rc;
+    return nr_mlp_backward_reduce(cfg, M, workspace, g_params, stream);
 }
 
 }  // extern "C"

@@ -3,15 +3,16 @@
 // Everything the host entry points and the kernels agree on lives here:
 //   * the flat fp32 parameter layout (nn.Module.parameters() order),
 //   * the packed MFMA fragment images of W (forward) and W^T (backward),
-//   * the "saved" activations written by a training forward, and
-//   * the backward workspace (per-layer pre-activation gradients dz and the
-//     dW partial slabs).
-//
-// Sample tiles: 32 samples per tile (one MFMA column block).  Saved/workspace
-// tensors are tile-blocked and feature-major: element (sample m, feature f)
-// of a tensor with F (padded) features lives at  tile*F*32 + f*32 + (m%32),
-// so the dW GEMM, whose reduction runs over samples, loads 16-byte operand
-// fragments directly.  ReLU masks are bitmasks in accumulator-register order.
+//     stored chunk-major: one chunk = every row block of one 32-wide k block,
+//     i.e. exactly what the kernels stream through LDS per step, each
+//     direction's images laid out in its stream order;
+//   * fp32 vectors (biases, w_sigma, W_rgb) in accumulator-register order;
+//   * the activations saved by a training forward and the per-layer
+//     pre-activation gradients dz written by the backward, both stored as
+//     MFMA B-operand images: per 32-sample tile and 32-feature block, FPB
+//     wave-wide 1-KB fragments (lane L = sample + 32*h holds 16 B), so every
+//     store is a fully coalesced 1-KB wave write.
+// ReLU masks are bitmasks in accumulator-register order (16 B per lane per layer).
 #pragma once
 
 #include <cstdint>
@@ -25,7 +26,7 @@ constexpr int kHB = kHidden / 32;      // hidden feature blocks
 constexpr int kMaxTrunk = 16;          // num_hidden_layers upper bound
 constexpr int kMaxMfmaLayers = kMaxTrunk + 2;  // trunk + feature + dir
 constexpr int kFragBytes = 1024;       // one wave-wide 16-B-per-lane operand fragment
-constexpr int kMaxJobs = kMaxTrunk + 4;  // dW jobs: trunk + feat + dir + sigma + rgb
+constexpr int kMaxJobs = kMaxTrunk + 3;  // dW jobs: trunk + (feat & sigma) + dir + rgb
 constexpr int kMaxSeg = 2;
 
 // One input segment of a linear layer: columns [col0, col0+width) of W,
@@ -41,26 +42,37 @@ struct LinearDesc {
     int nseg;
     Seg seg[kMaxSeg];
     int64_t pk_fwd, pk_bwd;  // byte offsets of the W / W^T fragment images
+    int64_t vb;              // byte offset of the bias vector image (accumulator order)
 };
 
-// A dW job: gradient of one linear layer (heads included) from the saved
-// input activations and the workspace dz.
+// A tensor range of a dW job: `blocks` consecutive 32-feature blocks of
+// saved (is_ws = 0) or workspace (is_ws = 1) tensor `tensor`.
+struct DwSeg {
+    int is_ws, tensor, blocks;
+};
+
+// A dW job: gradients of the linear layers whose dz blocks are `dz` and whose
+// input blocks are `in`.  Output slab per chunk: (NBz*32) x (KB*32 + 1) floats,
+// the last column holding the bias partial.
 struct DwJob {
-    int layer;                 // index into MlpPlan::lin (sigma/rgb heads: kSigma/kRgb)
-    int dz_tensor;             // workspace tensor holding dz (feature-major, F = NBz*32)
-    int dz_row0;               // first dz row of this job inside that tensor (heads block)
-    int rows;                  // valid output rows (out features)
-    int NB;                    // output blocks computed
-    int nin;                   // number of input tensors (segments)
-    int in_tensor[kMaxSeg];    // saved tensor ids per segment
-    int in_blocks[kMaxSeg];    // 32-blocks per segment
-    int KB;                    // total input blocks
-    int64_t slab_off;          // float offset of this job's slab (per chunk: NB*32*(KB*32+1))
+    int ndz, nin;
+    DwSeg dz[kMaxSeg], in[kMaxSeg];
+    int NBz, KB;
+    int64_t slab_off;  // float offset of this job's slab inside one chunk's slab set
 };
 
 // Saved tensor ids (training forward) and workspace tensor ids (backward).
 enum SavedId { SV_XENC = 0, SV_H0 = 1 /* .. SV_H0+n_layers-1 */ };
 enum WsId { WS_DZ0 = 0 /* dz of trunk i: WS_DZ0+i; then feat, dir, heads */ };
+
+// Per-parameter-range map for the slab reduction: parameters [p0, p0+rows*in)
+// are W rows `row0..` of a job slab, and [b0, b0+rows) its bias column.
+struct ReduceRange {
+    int job, row0, rows, in;
+    int64_t w_off, b_off;
+    int nseg;
+    int seg_col0[kMaxSeg], seg_w[kMaxSeg], seg_blk0[kMaxSeg];
+};
 
 struct MlpPlan {
     int L, Ld, n_layers, use_vd, prec;
@@ -71,7 +83,9 @@ struct MlpPlan {
     LinearDesc lin[kMaxMfmaLayers];   // [0, n_layers) trunk, n_layers feat, n_layers+1 dir
     int64_t sig_w, sig_b, rgb_w, rgb_b;
     int64_t packed_bytes;
+    int64_t vsig, vrgb;               // byte offsets of the w_sigma / W_rgb vector images
     int esize;                        // bytes per saved/workspace element (2 bf16, 4 fp32)
+    int fpb;                          // 1-KB fragments per 32x32 block (2 bf16, 4 fp32)
     // saved tensors
     int n_saved;                      // xenc, h0..h_{n-1}, feat, denc, hc
     int sv_feat, sv_denc, sv_hc;
@@ -81,10 +95,12 @@ struct MlpPlan {
     int n_ws;                         // dz_0..dz_{n-1}, dz_feat, dz_dir, dz_heads
     int ws_feat, ws_dir, ws_heads;
     int ws_F[kMaxTrunk + 3];
-    // dW jobs
+    // dW jobs and the reduction map
     int n_jobs;
     DwJob job[kMaxJobs];
     int64_t slab_floats_per_chunk;
+    int n_red;
+    ReduceRange red[kMaxJobs + 2];
 };
 
 inline bool is_skip(const MlpPlan& p, int i) { return (p.skips >> i) & 1u; }

@@ -18,7 +18,8 @@ from typing import Optional
 
 import torch
 
-_LIB_PATH = Path(__file__).resolve().parent / "lib" / "libnerf_hip.so"
+# NR_HIP_LIB selects another build of the same library (kernel-variant experiments).
+_LIB_PATH = Path(os.environ.get("NR_HIP_LIB") or Path(__file__).resolve().parent / "lib" / "libnerf_hip.so")
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -74,6 +75,10 @@ _SIGNATURES = {
     "nr_mlp_forward": (c_i, [_cfg_p, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "nr_mlp_backward": (c_i, [_cfg_p, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "nr_mlp_backward_dx": (c_i, [_cfg_p, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                 c_vp, c_vp]),
+    "nr_mlp_backward_dw": (c_i, [_cfg_p, c_i64, c_vp, c_vp, c_vp]),
+    "nr_mlp_backward_reduce": (c_i, [_cfg_p, c_i64, c_vp, c_vp, c_vp]),
     "nr_sumsq": (c_i, [c_vp, c_i64, c_vp, c_vp]),
     "nr_adam_step": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_d, c_d, c_d, c_d, c_i64, c_vp, c_f, c_vp]),
     "nr_expand_viewdirs": (c_i, [c_vp, c_i, c_i, c_vp, c_vp]),

@@ -99,9 +99,11 @@ class _MLPFunction(torch.autograd.Function):
         g_d = torch.empty(M, 3, device=dev) if (ctx.needs_input_grad[1] and ctx.has_d) else None
         if M > 0:
             ws = torch.empty(int(_hip.load().nr_mlp_workspace_bytes(cfg, M)), device=dev, dtype=torch.uint8)
-            call("nr_mlp_backward", cfg, ptr(packed), ptr(flat), ptr(xc), ptr(dc) if ctx.has_d else None, M, ptr(rgb),
-                 ptr(sigma), ptr(saved), ptr(g_rgb), ptr(g_sigma), ptr(gflat), ptr(g_x), ptr(g_d), ptr(ws),
-                 _hip.stream_ptr(), tag=f"[M={M}]")
+            st, tag = _hip.stream_ptr(), f"[M={M}]"
+            call("nr_mlp_backward_dx", cfg, ptr(packed), ptr(flat), ptr(xc), ptr(dc) if ctx.has_d else None, M,
+                 ptr(rgb), ptr(sigma), ptr(saved), ptr(g_rgb), ptr(g_sigma), ptr(g_x), ptr(g_d), ptr(ws), st, tag=tag)
+            call("nr_mlp_backward_dw", cfg, M, ptr(saved), ptr(ws), st, tag=tag)
+            call("nr_mlp_backward_reduce", cfg, M, ptr(ws), ptr(gflat), st, tag=tag)
         else:
             gflat.zero_()
         grads = []
