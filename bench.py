@@ -33,8 +33,48 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "training rays/sec + test PSNR, lego 800² 64c+128f, at 1/2/4/8 MI355X"
-MACS_PER_EVAL = 593_408
+MACS_PER_EVAL = 593_408  # MLP multiply-adds per sample (forward)
 PEAK_TFLOPS = {"bf16": 2516.6, "fp32": 157.3}  # dense MFMA (256 CU x 2.4 GHz); MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0  # HBM3E spec peak; MI355X_MICROARCH.md (~6300 achievable)
+
+# Algorithmic work per sample of each fused-MLP kernel (default 8x256 model, L=10/4):
+#   forward: every linear layer's multiply-adds (MFMA-bound);
+#   backward dX: the W^T products of the dX chain without the x_enc rows (no g_x in training);
+#   dW: it must read every saved layer input and every dz once (HBM-bound; unpadded widths).
+MACS_DX = 128 * (256 + 27) + 256 * 256 + 7 * 256 * 256
+DW_FEATURES = (63 + 8 * 256 + 256 + 27 + 128) + (8 * 256 + 256 + 128 + 1 + 3)
+KERNEL_OF = {"nr_mlp_forward": "mlp_fwd_kernel", "nr_mlp_backward_dx": "mlp_bwd_kernel",
+             "nr_mlp_backward_dw": "mlp_dw_kernel", "nr_mlp_backward_reduce": "mlp_dw_reduce_kernel"}
+
+
+def traffic_of(kernel: str, M: int, prec: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
+    (profiles/traffic.json, written by tools/traffic.py: 2 x FETCH_SIZE + WRITE_SIZE,
+    the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md), or None."""
+    f = ROOT / "profiles" / "traffic.json"
+    if not f.exists():
+        return None
+    for rec in json.loads(f.read_text()).get("kernels", []):
+        if rec["kernel"] == kernel and rec["M"] == M and rec["precision"] == prec:
+            return rec["bytes_per_launch"]
+    return None
+
+
+def roofline_of(entry: str, M: int, ms: float, prec: str, n_params: int):
+    """(bound, achieved, peak, unit, work-per-launch description) of one fused-MLP launch."""
+    esize = 2 if prec == "bf16" else 4
+    if entry == "nr_mlp_forward":
+        return "mfma", 2.0 * MACS_PER_EVAL * M / (ms * 1e-3) / 1e12, PEAK_TFLOPS[prec], "TFLOP/s", \
+            f"2 x {MACS_PER_EVAL} MAC x {M} samples"
+    if entry == "nr_mlp_backward_dx":
+        return "mfma", 2.0 * MACS_DX * M / (ms * 1e-3) / 1e12, PEAK_TFLOPS[prec], "TFLOP/s", \
+            f"2 x {MACS_DX} MAC x {M} samples"
+    if entry == "nr_mlp_backward_dw":
+        nbytes = DW_FEATURES * esize * M + 4 * n_params
+        return "hbm", nbytes / (ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s", \
+            f"{DW_FEATURES} features x {esize} B x {M} samples + {n_params} fp32 grads"
+    nbytes = 4 * n_params * 2
+    return "hbm", nbytes / (ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s", f"{n_params} fp32 grads"
 
 
 def lego_rays(n_rays: int, seed: int, device):
@@ -143,12 +183,11 @@ def main():
         dt = float(tt)
 
     calls = timer.summary()
-    Mf = B * (rcfg.num_samples + rcfg.num_samples_fine)
-    key = f"nr_mlp_forward[M={Mf}]"
-    n_launch, ms = calls[key]
-    flops = 2.0 * MACS_PER_EVAL * Mf
-    peak = PEAK_TFLOPS[args.precision]
-    achieved = flops / (ms * 1e-3) / 1e12
+    # dominant kernel = largest total time over the timed region
+    dom_key = max(calls, key=lambda k: calls[k][0] * calls[k][1])
+    n_launch, ms = calls[dom_key]
+    entry, M = dom_key.split("[M=")[0], int(dom_key.split("[M=")[1].rstrip("]"))
+    bound, achieved, peak, unit, work = roofline_of(entry, M, ms, args.precision, mf.flat_params().numel())
     value = world * B * args.steps / dt
     out = {
         "metric": METRIC,
@@ -171,13 +210,14 @@ def main():
             "parallelism": f"dp{world}",
         },
         "roofline": {
-            "bound": "mfma",
-            "kernel": f"mlp_fwd_kernel (fine net, M={Mf} samples, training mode)",
+            "bound": bound,
+            "kernel": f"{KERNEL_OF.get(entry, entry)} via {entry} (M={M} samples, fine net)",
             "achieved": round(achieved, 2),
             "peak": peak,
-            "unit": "TFLOP/s",
+            "unit": unit,
             "frac": round(achieved / peak, 4),
-            "traffic": None,
+            "traffic": traffic_of(KERNEL_OF.get(entry, entry), M, args.precision),
+            "work_per_launch": work,
             "launch_ms": round(ms, 4),
             "launches": n_launch,
         },

@@ -1,0 +1,106 @@
+"""Summarise a rocprofv3 run for profiles/: per-(kernel, grid) launch durations
+from the kernel trace, and HBM traffic per launch from the two PMC passes.
+
+    python tools/prof_summary.py gpurun_out ROUND_TAG
+
+reads  gpurun_out/prof/run_kernel_trace.csv
+       gpurun_out/pmc_fetch/run_counter_collection.csv   (FETCH_SIZE, KB)
+       gpurun_out/pmc_write/run_counter_collection.csv   (WRITE_SIZE, KB)
+writes profiles/<tag>_kernel_summary.csv and profiles/traffic.json.
+
+Traffic = 2 x FETCH_SIZE + WRITE_SIZE: on gfx950 FETCH_SIZE counts exactly half of
+the bytes of 16-B-per-lane streaming reads (MI355X_MICROARCH.md, HBM section),
+WRITE_SIZE counts 16-B streaming stores exactly.  Both count Infinity-Cache hits.
+"""
+
+from __future__ import annotations
+
+import csv
+import json
+import re
+import statistics
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+# fused-MLP grid size (workgroups x threads) -> samples M, per kernel family
+FAMILIES = {"mlp_fwd_kernel": "nr_mlp_forward", "mlp_bwd_kernel": "nr_mlp_backward_dx",
+            "mlp_dw_kernel": "nr_mlp_backward_dw", "mlp_dw_reduce_kernel": "nr_mlp_backward_reduce"}
+
+
+def short(name: str) -> str:
+    m = re.search(r"nr::(\w+)", name)
+    return m.group(1) if m else name.split("(")[0]
+
+
+def precision_of(name: str) -> str:
+    m = re.search(r"nr::mlp_\w+_kernel<(\d)", name)
+    return {"1": "bf16", "0": "fp32"}.get(m.group(1), "") if m else ""
+
+
+def sample_count(name: str, grid: int, last_M: int) -> int:
+    """M of a fused-MLP launch: the forward/backward kernels run one 32-sample tile per
+    wave; dW and its reduction follow the backward launch of the same M in the stream."""
+    fam = short(name)
+    if fam in ("mlp_fwd_kernel", "mlp_bwd_kernel"):
+        return grid // 64 * 32
+    if fam in ("mlp_dw_kernel", "mlp_dw_reduce_kernel"):
+        return last_M
+    return 0
+
+
+def main(out_dir: str, tag: str) -> None:
+    base = Path(out_dir)
+    rows = defaultdict(list)
+    with open(base / "prof" / "run_kernel_trace.csv") as f:
+        trace = sorted(csv.DictReader(f), key=lambda r: int(r["Dispatch_Id"]))
+    last_M = 0
+    for r in trace:
+        grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        M = sample_count(r["Kernel_Name"], grid, last_M)
+        last_M = M or last_M
+        rows[(r["Kernel_Name"], grid, M)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    summ = ROOT / "profiles" / f"{tag}_kernel_summary.csv"
+    with open(summ, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "grid_threads", "M_samples", "calls", "avg_ms", "median_ms", "total_ms"])
+        for (k, g, M), v in sorted(rows.items(), key=lambda kv: -sum(kv[1])):
+            w.writerow([short(k), g, M or "", len(v), f"{statistics.mean(v):.4f}", f"{statistics.median(v):.4f}",
+                        f"{sum(v):.3f}"])
+    print(f"wrote {summ}")
+
+    counters = defaultdict(lambda: defaultdict(list))
+    for sub, cname in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+        p = base / sub / "run_counter_collection.csv"
+        if not p.exists():
+            continue
+        with open(p) as f:
+            recs_ = sorted((r for r in csv.DictReader(f) if r["Counter_Name"] == cname),
+                           key=lambda r: int(r["Dispatch_Id"]))
+        last_M = 0
+        for r in recs_:
+            M = sample_count(r["Kernel_Name"], int(r["Grid_Size"]), last_M)
+            last_M = M or last_M
+            key = (r["Kernel_Name"], M)
+            counters[key][cname].append(float(r["Counter_Value"]) * 1024.0)  # KB -> B
+    recs = []
+    for (k, M), c in sorted(counters.items()):
+        fam = short(k)
+        if fam not in FAMILIES or "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+            continue
+        fetch = statistics.median(c["FETCH_SIZE"])
+        write = statistics.median(c["WRITE_SIZE"])
+        recs.append({"kernel": fam, "entry": FAMILIES[fam], "precision": precision_of(k), "M": M,
+                     "fetch_size_bytes": fetch, "write_size_bytes": write,
+                     "bytes_per_launch": 2.0 * fetch + write, "launches": len(c["FETCH_SIZE"])})
+    out = {"source": f"profiles/{tag}: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
+                     "python bench.py --steps 2 --warmup 1; traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (median)",
+           "kernels": recs}
+    (ROOT / "profiles" / "traffic.json").write_text(json.dumps(out, indent=1))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
