@@ -221,6 +221,9 @@ def main():
             "launch_ms": round(ms, 4),
             "launches": n_launch,
         },
+        # whole-step MFMA fraction: rays/s x training FLOP/ray / (GPUs x peak)
+        "step_mfma_frac": round(value * 6 * MACS_PER_EVAL * (2 * rcfg.num_samples + rcfg.num_samples_fine)
+                                / (world * PEAK_TFLOPS[args.precision] * 1e12), 4),
         "kernel_ms": {k: round(v[1], 4) for k, v in calls.items()},
         "final_loss": round(loss, 6),
         "psnr": None,

@@ -106,6 +106,10 @@ class _MLPFunction(torch.autograd.Function):
             call("nr_mlp_backward_reduce", cfg, M, ptr(ws), ptr(gflat), st, tag=tag)
         else:
             gflat.zero_()
+        if net._grad_ready_hook is not None:
+            # data parallel: start this net's gradient all-reduce now, overlapping the
+            # rest of the backward (the fine net finishes before the coarse one)
+            net._grad_ready_hook(gflat)
         grads = []
         off = 0
         for p in net._param_list:
@@ -153,6 +157,8 @@ class NeRF(nn.Module):
         self._flat: Optional[torch.Tensor] = None
         self._packed: Optional[torch.Tensor] = None
         self._packed_key = None
+        # called with the flat gradient as soon as the backward has produced it
+        self._grad_ready_hook = None
 
     # -- flat parameter buffer -------------------------------------------------
     @property
