@@ -33,9 +33,6 @@
 
 namespace nr {
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / 64;
-
 template <int PREC>
 struct InBlk;
 template <>
@@ -748,73 +745,77 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
 }
 
 // ------------------------------------------------------------------ dW ----
-// Workgroup = (job, chunk of tiles, group of up to 4 sub-grids of 4x4 blocks).
-// Per tile the job's dz and input blocks are staged in LDS (double buffered,
-// LDS-DMA in 1-KB wave pieces); each wave accumulates its sub-grid with
-// operands rebuilt sample-major from the B-operand images.  Output slab per
-// chunk: [dz row][input col | bias] fp32.
+// Workgroup = (job, chunk of tiles): 8 waves, each accumulating a 4x2-block
+// sub-grid of the job's NBz x KB output grid (<= 64 blocks).  Per tile the job's
+// dz and input blocks are staged into LDS by LDS-DMA (double buffered, 1-KB wave
+// pieces) and the sample-major MFMA operands are rebuilt from the B-operand
+// images.  Output slab per chunk: [dz row][input col | bias] fp32.
+constexpr int kDwThreads = 512;
+constexpr int kDwWaves = kDwThreads / 64;
+constexpr int kDwP = 4, kDwQ = 2;  // blocks per wave: dz rows x input cols
+
 struct DwArgs {
-    const char* saved;
-    const char* ws;
     float* slabs;
     int64_t tiles;
-    int tiles_per_chunk;
-    int n_jobs;
-    int stage_bytes;
-    int job_wg0[kMaxJobs + 1];
-    int job_sg[kMaxJobs], job_nbg[kMaxJobs], job_groups[kMaxJobs];
-    int job_NBz[kMaxJobs], job_KB[kMaxJobs];
-    int job_nseg[kMaxJobs];                   // dz segments then input segments
-    int64_t seg_off[kMaxJobs][2 * kMaxSeg];   // byte offset of the tensor region
-    int seg_blocks[kMaxJobs][2 * kMaxSeg];
-    int seg_isws[kMaxJobs][2 * kMaxSeg];
-    int64_t job_slab[kMaxJobs];
+    int tiles_per_chunk, chunks;
+    int stage_bytes, nstage;
     int64_t slab_floats_per_chunk;
+    int job_NBz[kMaxJobs], job_KB[kMaxJobs], job_nbg[kMaxJobs], job_waves[kMaxJobs], job_nseg[kMaxJobs];
+    int64_t job_slab[kMaxJobs];
+    const char* seg_ptr[kMaxJobs][2 * kMaxJobSeg];  // tensor region: dz segments, then inputs
+    int seg_blocks[kMaxJobs][2 * kMaxJobSeg];  // int: scalar-loadable
 };
 
 // Block-local feature of dW operand row/col index r: r = 16h + i <-> accumulator
 // register i of lane half h in the B-operand image.
 __device__ __forceinline__ int dw_feat(int r) { return acc_row(r & 15, r >> 4); }
 
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+// bf16 staging swizzle: image lane L of fragment s sits in LDS slot
+// L ^ 4*(L>>5 & 1) ^ 8*s (an involution), which makes the transpose reads of
+// dw_frag_bf16 bank-conflict free (the 16 slots a 32-lane half reads are
+// distinct mod 16).  glds writes lane-linear, so the swizzle goes on the source.
+__device__ __forceinline__ int dw_slot(int L, int s) { return L ^ (((L >> 5) & 1) << 2) ^ (s << 3); }
 
-// bf16 operand of k-step ks (16 samples) from a staged block image [s][L][8]:
-// lane l = 16g + i (h = g&1, hh = g>>1) receives feature acc_row(i, h) of
-// samples 16ks + 8hh + 0..7, via two transpose reads of 4 samples x 16 features
-// (lane 4q+p of the group addresses sample q, features 4p..4p+3, cdna_hip T10).
-__device__ __forceinline__ bf16x8 dw_frag_bf16(const char* blk, int ks, int lane) {
-    const int g = lane >> 4, h = g & 1, hh = g >> 1;
-    const int lam = lane & 15, q = lam >> 2, p = lam & 3;
-    const int s = p >> 1;
-    const int m0 = 16 * ks + 8 * hh + q;
-    const char* a0 = blk + (s * 64 + m0 + 32 * h) * 16 + 8 * (p & 1);
-    const char* a1 = a0 + 4 * 16;
-    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+// ds_read_b64_tr_b16 through inline asm: the builtin makes hipcc wait vmcnt(0)
+// (every in-flight LDS-DMA stage) before each read, which would serialise the
+// staging pipeline.  The caller waits lgkmcnt itself (tr_wait) before use.
+template <int OFF>
+__device__ __forceinline__ void tr16(uint64_t& out, uint32_t addr) {
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(out) : "v"(addr), "i"(OFF));
+}
+
+__device__ __forceinline__ bf16x8 tr_pair(uint64_t lo, uint64_t hi) {
     bf16x8 r;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        r[j] = __builtin_bit_cast(__bf16, lo[j]);
-        r[4 + j] = __builtin_bit_cast(__bf16, hi[j]);
+        r[j] = __builtin_bit_cast(__bf16, static_cast<unsigned short>(lo >> (16 * j)));
+        r[4 + j] = __builtin_bit_cast(__bf16, static_cast<unsigned short>(hi >> (16 * j)));
     }
     return r;
 }
 
+// LDS byte offsets, within a staged block, of the two transpose reads that give
+// lane l its bf16 operand for k-step ks: lane l = 16g + i (h = g&1, hh = g>>1)
+// receives feature acc_row(i, h) of samples 16ks + 8hh + 0..7 (two reads of 4
+// samples x 16 features; lane 4q+p of a group addresses sample q, features
+// 4p..4p+3: cdna_hip_programming.md T10).
+__device__ __forceinline__ uint32_t dw_tr_off(int ks, int half, int lane) {
+    const int g = lane >> 4, h = g & 1, hh = g >> 1;
+    const int lam = lane & 15, q = lam >> 2, p = lam & 3;
+    const int s = p >> 1;
+    const int L = 16 * ks + 8 * hh + q + 32 * h + 4 * half;
+    return static_cast<uint32_t>(s * kFragBytes + dw_slot(L, s) * 16 + 8 * (p & 1));
+}
+
 template <int PREC>
-__global__ __launch_bounds__(kThreads, 1) void mlp_dw_kernel(DwArgs a) {
+__global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int wg = blockIdx.x;
-    int j = 0;
-    while (j + 1 < a.n_jobs && wg >= a.job_wg0[j + 1]) ++j;
-    const int groups = a.job_groups[j];
-    const int local = wg - a.job_wg0[j];
-    const int chunk = local / groups;
-    const int sg = (local % groups) * kWaves + wv;
-    const bool active = sg < a.job_sg[j];
-    const int nbg = active ? sg % a.job_nbg[j] : 0, kbg = active ? sg / a.job_nbg[j] : 0;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar staging loop
+    const int j = blockIdx.x / a.chunks, chunk = blockIdx.x % a.chunks;
     const int NBz = a.job_NBz[j], KB = a.job_KB[j];
+    const bool active = wv < a.job_waves[j];
+    const int nbg = active ? wv % a.job_nbg[j] : 0, kbg = active ? wv / a.job_nbg[j] : 0;
     const int64_t t0 = static_cast<int64_t>(chunk) * a.tiles_per_chunk;
     int64_t t1 = t0 + a.tiles_per_chunk;
     if (t1 > a.tiles) t1 = a.tiles;
@@ -822,62 +823,105 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_dw_kernel(DwArgs a) {
     constexpr int BLK = FPB * kFragBytes;
     const int nseg = a.job_nseg[j];
 
-    // stage tile t into buffer b (the job's blocks, dz segments first)
+    // Stage tile t into buffer b (the job's blocks, dz segments first).  Every wave
+    // issues exactly `per_wave` 1-KB LDS-DMA pieces per tile (padding pieces re-load
+    // piece 0 into a scratch KB), so a counted vmcnt can retire one stage while the
+    // next NS-2 stay in flight across the barrier.
+    const int total = (NBz + KB) * FPB;
+    const int per_wave = (total + kDwWaves - 1) / kDwWaves;
     auto stage = [&](int64_t t, int b) {
         char* dst = lds + b * a.stage_bytes;
-        int blk0 = 0;
-        for (int s = 0; s < nseg; ++s) {
-            const int nb = a.seg_blocks[j][s];
-            const char* src = (a.seg_isws[j][s] ? a.ws : a.saved) + a.seg_off[j][s] + t * nb * BLK;
-            const int pieces = nb * FPB;  // 1-KB wave pieces
-            for (int pc = wv; pc < pieces; pc += kWaves)
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(src + pc * kFragBytes + lane * 16),
-                    (__attribute__((address_space(3))) void*)(dst + (blk0 * FPB + pc) * kFragBytes), 16, 0, 0);
-            blk0 += nb;
+        for (int k = 0; k < per_wave; ++k) {
+            int pc = wv + k * kDwWaves;
+            char* d = lds + a.nstage * a.stage_bytes;  // scratch KB for padding pieces
+            if (pc >= total) pc = 0;
+            else d = dst + pc * kFragBytes;
+            int sg = 0, p0 = 0;
+            while (pc >= p0 + a.seg_blocks[j][sg] * FPB) p0 += a.seg_blocks[j][sg++] * FPB;
+            const int nb = a.seg_blocks[j][sg];
+            const char* src = a.seg_ptr[j][sg] + t * nb * BLK + (pc - p0) * kFragBytes;
+            const int L = PREC == NR_PREC_BF16 ? dw_slot(lane, (pc - p0) % FPB) : lane;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + L * 16),
+                                             (__attribute__((address_space(3))) void*)(d), 16, 0, 0);
+        }
+    };
+    // wait until at most n of this wave's pieces are outstanding (n: wave-uniform)
+    auto wait_pieces = [](int n) {
+        switch (n) {
+            case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+            case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+            case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+            case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+            default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
         }
     };
 
-    f32x16 acc[4][4];
+    f32x16 acc[kDwP][kDwQ];
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int p = 0; p < kDwP; ++p)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) zero(acc[p][q]);
-    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-    bool nval[4], kval[4];
+        for (int q = 0; q < kDwQ; ++q) zero(acc[p][q]);
+    float bsum[kDwP] = {0.f, 0.f, 0.f, 0.f};
+    bool nval[kDwP], kval[kDwQ];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        nval[q] = active && 4 * nbg + q < NBz;
-        kval[q] = active && 4 * kbg + q < KB;
-    }
+    for (int p = 0; p < kDwP; ++p) nval[p] = active && kDwP * nbg + p < NBz;
+#pragma unroll
+    for (int q = 0; q < kDwQ; ++q) kval[q] = active && kDwQ * kbg + q < KB;
     const bool do_bias = active && kbg == 0;
 
-    if (t0 < t1) stage(t0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    uint32_t trof[2][2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) trof[ks][hf] = dw_tr_off(ks, hf, lane);
+
+    const int NS = a.nstage;
+    for (int k = 0; k < NS - 1; ++k)
+        if (t0 + k < t1) stage(t0 + k, k);
     for (int64_t t = t0; t < t1; ++t) {
-        const int cur = static_cast<int>((t - t0) & 1);
-        if (t + 1 < t1) stage(t + 1, cur ^ 1);
-        const char* buf = lds + cur * a.stage_bytes;
+        // stages t+1 .. t+NS-2 may stay in flight
+        int64_t ahead = t1 - 1 - t;
+        if (ahead > NS - 2) ahead = NS - 2;
+        wait_pieces(per_wave * static_cast<int>(ahead));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (t + NS - 1 < t1) stage(t + NS - 1, static_cast<int>((t + NS - 1 - t0) % NS));
+        const char* buf = lds + static_cast<int>((t - t0) % NS) * a.stage_bytes;
         if (active) {
             if constexpr (PREC == NR_PREC_BF16) {
+                const uint32_t bufA = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf)) + kDwP * nbg * BLK;
+                const uint32_t bufB = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf)) +
+                                      (NBz + kDwQ * kbg) * BLK;
 #pragma unroll
                 for (int ks = 0; ks < 2; ++ks) {
-                    bf16x8 A[4], Bm[4];
+                    uint64_t ra[kDwP][2], rb[kDwQ][2];
 #pragma unroll
-                    for (int p = 0; p < 4; ++p)
-                        if (nval[p]) A[p] = dw_frag_bf16(buf + (4 * nbg + p) * BLK, ks, lane);
+                    for (int hf = 0; hf < 2; ++hf) {
+                        const uint32_t oa = bufA + trof[ks][hf], ob = bufB + trof[ks][hf];
+                        tr16<0 * BLK>(ra[0][hf], oa);
+                        tr16<1 * BLK>(ra[1][hf], oa);
+                        tr16<2 * BLK>(ra[2][hf], oa);
+                        tr16<3 * BLK>(ra[3][hf], oa);
+                        tr16<0 * BLK>(rb[0][hf], ob);
+                        tr16<1 * BLK>(rb[1][hf], ob);
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)"
+                                 : "+v"(ra[0][0]), "+v"(ra[0][1]), "+v"(ra[1][0]), "+v"(ra[1][1]), "+v"(ra[2][0]),
+                                   "+v"(ra[2][1]), "+v"(ra[3][0]), "+v"(ra[3][1]), "+v"(rb[0][0]), "+v"(rb[0][1]),
+                                   "+v"(rb[1][0]), "+v"(rb[1][1]));
+                    bf16x8 A[kDwP], Bm[kDwQ];
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (kval[q]) Bm[q] = dw_frag_bf16(buf + (NBz + 4 * kbg + q) * BLK, ks, lane);
+                    for (int p = 0; p < kDwP; ++p) A[p] = tr_pair(ra[p][0], ra[p][1]);
 #pragma unroll
-                    for (int p = 0; p < 4; ++p) {
+                    for (int q = 0; q < kDwQ; ++q) Bm[q] = tr_pair(rb[q][0], rb[q][1]);
+#pragma unroll
+                    for (int p = 0; p < kDwP; ++p) {
                         if (!nval[p]) continue;
                         if (do_bias)
 #pragma unroll
                             for (int e = 0; e < 8; ++e) bsum[p] += static_cast<float>(A[p][e]);
 #pragma unroll
-                        for (int q = 0; q < 4; ++q)
+                        for (int q = 0; q < kDwQ; ++q)
                             if (kval[q]) acc[p][q] = mfma_bf16(A[p], Bm[q], acc[p][q]);
                     }
                 }
@@ -889,50 +933,48 @@ __global__ __launch_bounds__(kThreads, 1) void mlp_dw_kernel(DwArgs a) {
 #pragma unroll 4
                 for (int ss = 0; ss < 16; ++ss) {
                     const int m = 2 * ss + kk;
-                    float A[4], Bv[4];
+                    float A[kDwP], Bv[kDwQ];
 #pragma unroll
-                    for (int p = 0; p < 4; ++p)
-                        A[p] = nval[p] ? *reinterpret_cast<const float*>(buf + (4 * nbg + p) * BLK + off + m * 16)
+                    for (int p = 0; p < kDwP; ++p)
+                        A[p] = nval[p] ? *reinterpret_cast<const float*>(buf + (kDwP * nbg + p) * BLK + off + m * 16)
                                        : 0.f;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        Bv[q] = kval[q] ? *reinterpret_cast<const float*>(buf + (NBz + 4 * kbg + q) * BLK + off +
+                    for (int q = 0; q < kDwQ; ++q)
+                        Bv[q] = kval[q] ? *reinterpret_cast<const float*>(buf + (NBz + kDwQ * kbg + q) * BLK + off +
                                                                           m * 16)
                                         : 0.f;
 #pragma unroll
-                    for (int p = 0; p < 4; ++p) {
+                    for (int p = 0; p < kDwP; ++p) {
                         if (!nval[p]) continue;
                         if (do_bias) bsum[p] += A[p];
 #pragma unroll
-                        for (int q = 0; q < 4; ++q)
+                        for (int q = 0; q < kDwQ; ++q)
                             if (kval[q]) acc[p][q] = mfma_f32(A[p], Bv[q], acc[p][q]);
                     }
                 }
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
     }
     if (!active) return;
     float* slab = a.slabs + static_cast<int64_t>(chunk) * a.slab_floats_per_chunk + a.job_slab[j];
     const int ld = KB * 32 + 1;
     const int hl = lane >> 5, ml = lane & 31;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < kDwP; ++p) {
         if (!nval[p]) continue;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < kDwQ; ++q) {
             if (!kval[q]) continue;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = 32 * (4 * nbg + p) + dw_feat(acc_row(r, hl));
-                const int col = 32 * (4 * kbg + q) + dw_feat(ml);
+                const int row = 32 * (kDwP * nbg + p) + dw_feat(acc_row(r, hl));
+                const int col = 32 * (kDwQ * kbg + q) + dw_feat(ml);
                 slab[static_cast<int64_t>(row) * ld + col] = acc[p][q][r];
             }
         }
         if (do_bias) {
             const float tot = bsum[p] + __shfl_xor(bsum[p], 32);
-            if (hl == 0) slab[static_cast<int64_t>(32 * (4 * nbg + p) + dw_feat(ml)) * ld + KB * 32] = tot;
+            if (hl == 0) slab[static_cast<int64_t>(32 * (kDwP * nbg + p) + dw_feat(ml)) * ld + KB * 32] = tot;
         }
     }
 }
@@ -945,39 +987,42 @@ struct ReduceArgs {
     int chunks;
     int64_t slab_floats_per_chunk;
     int n_red;
-    int red_row0[kMaxJobs + 2], red_rows[kMaxJobs + 2], red_in[kMaxJobs + 2], red_KB[kMaxJobs + 2];
-    int64_t red_w_off[kMaxJobs + 2], red_b_off[kMaxJobs + 2], red_slab[kMaxJobs + 2];
-    int red_nseg[kMaxJobs + 2];
-    int red_seg_col0[kMaxJobs + 2][kMaxSeg], red_seg_w[kMaxJobs + 2][kMaxSeg], red_seg_blk0[kMaxJobs + 2][kMaxSeg];
+    int rows[kMaxRed], in[kMaxRed], nseg[kMaxRed], bjob[kMaxRed], brow0[kMaxRed];
+    int64_t w_off[kMaxRed], b_off[kMaxRed];
+    RedSeg seg[kMaxRed][kMaxSeg];
+    int64_t job_slab[kMaxJobs];
+    int job_KB[kMaxJobs];
 };
 
 __global__ void mlp_dw_reduce_kernel(ReduceArgs a) {
     const int64_t pidx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (pidx >= a.param_count) return;
-    int q = -1;
-    int64_t row = 0, col = -1;
-    for (int k = 0; k < a.n_red; ++k) {
-        const int64_t wsz = static_cast<int64_t>(a.red_rows[k]) * a.red_in[k];
-        if (pidx >= a.red_w_off[k] && pidx < a.red_w_off[k] + wsz) {
-            q = k;
-            const int64_t e = pidx - a.red_w_off[k];
-            row = e / a.red_in[k];
-            const int c = static_cast<int>(e % a.red_in[k]);
-            for (int s = 0; s < a.red_nseg[k]; ++s)
-                if (c >= a.red_seg_col0[k][s] && c < a.red_seg_col0[k][s] + a.red_seg_w[k][s])
-                    col = 32 * a.red_seg_blk0[k][s] + (c - a.red_seg_col0[k][s]);
-            break;
-        }
-        if (pidx >= a.red_b_off[k] && pidx < a.red_b_off[k] + a.red_rows[k]) {
-            q = k;
-            row = pidx - a.red_b_off[k];
-            col = static_cast<int64_t>(a.red_KB[k]) * 32;
-            break;
+    int job = -1;
+    int64_t row = 0, col = 0;
+    for (int k = 0; k < a.n_red && job < 0; ++k) {
+        const int64_t wsz = static_cast<int64_t>(a.rows[k]) * a.in[k];
+        if (pidx >= a.w_off[k] && pidx < a.w_off[k] + wsz) {
+            const int64_t e = pidx - a.w_off[k];
+            const int r = static_cast<int>(e / a.in[k]);
+            const int c = static_cast<int>(e % a.in[k]);
+            for (int s = 0; s < a.nseg[k]; ++s) {
+                const RedSeg& sg = a.seg[k][s];
+                if (c >= sg.col0 && c < sg.col0 + sg.width) {
+                    job = sg.job;
+                    row = sg.slab_row0 + r;
+                    col = sg.slab_col0 + (c - sg.col0);
+                }
+            }
+            if (job < 0) return;
+        } else if (pidx >= a.b_off[k] && pidx < a.b_off[k] + a.rows[k]) {
+            job = a.bjob[k];
+            row = a.brow0[k] + (pidx - a.b_off[k]);
+            col = static_cast<int64_t>(a.job_KB[job]) * 32;
         }
     }
-    if (q < 0 || col < 0) return;
-    const int64_t ld = static_cast<int64_t>(a.red_KB[q]) * 32 + 1;
-    const float* s = a.slabs + a.red_slab[q] + (row + a.red_row0[q]) * ld + col;
+    if (job < 0) return;
+    const int64_t ld = static_cast<int64_t>(a.job_KB[job]) * 32 + 1;
+    const float* s = a.slabs + a.job_slab[job] + row * ld + col;
     float acc = 0.f;
     for (int c = 0; c < a.chunks; ++c) acc += s[static_cast<int64_t>(c) * a.slab_floats_per_chunk];
     a.g[pidx] = acc;
@@ -1349,52 +1394,54 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
     MlpPlan p;
     if (!plan_or_error(cfg, &p)) return NR_EARG;
     NR_REQUIRE(saved && workspace && M >= 0, "nr_mlp_backward_dw: null pointer");
+    NR_REQUIRE((reinterpret_cast<uintptr_t>(saved) & 15) == 0 && (reinterpret_cast<uintptr_t>(workspace) & 15) == 0,
+               "nr_mlp_backward_dw: saved and workspace must be 16-byte aligned");
     if (M == 0) return NR_OK;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const MlpSizes z = make_sizes(p, M);
+    const char* sv = static_cast<const char*>(saved);
     char* ws = static_cast<char*>(workspace);
     DwArgs w;
     std::memset(&w, 0, sizeof(w));
-    w.saved = static_cast<const char*>(saved);
-    w.ws = ws;
     w.slabs = reinterpret_cast<float*>(ws + z.slab_off);
     w.tiles = z.tiles;
+    w.chunks = z.chunks;
     w.tiles_per_chunk = static_cast<int>(ceil_div_ll(z.tiles, z.chunks));
-    w.n_jobs = p.n_jobs;
     w.slab_floats_per_chunk = p.slab_floats_per_chunk;
-    int wg = 0, max_blk = 0;
+    int max_blk = 0;
     for (int j = 0; j < p.n_jobs; ++j) {
         const DwJob& jb = p.job[j];
-        w.job_wg0[j] = wg;
-        w.job_nbg[j] = (jb.NBz + 3) / 4;
-        w.job_sg[j] = w.job_nbg[j] * ((jb.KB + 3) / 4);
-        w.job_groups[j] = (w.job_sg[j] + kWaves - 1) / kWaves;
-        wg += z.chunks * w.job_groups[j];
         w.job_NBz[j] = jb.NBz;
         w.job_KB[j] = jb.KB;
+        w.job_nbg[j] = ceil_div(jb.NBz, kDwP);
+        w.job_waves[j] = w.job_nbg[j] * ceil_div(jb.KB, kDwQ);
+        NR_REQUIRE(w.job_waves[j] <= kDwWaves, "nr_mlp_backward_dw: job %d grid %dx%d exceeds the workgroup", j,
+                   jb.NBz, jb.KB);
         int ns = 0;
         for (int q = 0; q < jb.ndz; ++q, ++ns) {
-            w.seg_off[j][ns] = (jb.dz[q].is_ws ? z.ws_off : z.saved_off)[jb.dz[q].tensor];
+            w.seg_ptr[j][ns] = (jb.dz[q].is_ws ? ws : sv) + (jb.dz[q].is_ws ? z.ws_off : z.saved_off)[jb.dz[q].tensor];
             w.seg_blocks[j][ns] = jb.dz[q].blocks;
-            w.seg_isws[j][ns] = jb.dz[q].is_ws;
         }
         for (int q = 0; q < jb.nin; ++q, ++ns) {
-            w.seg_off[j][ns] = (jb.in[q].is_ws ? z.ws_off : z.saved_off)[jb.in[q].tensor];
+            w.seg_ptr[j][ns] = (jb.in[q].is_ws ? ws : sv) + (jb.in[q].is_ws ? z.ws_off : z.saved_off)[jb.in[q].tensor];
             w.seg_blocks[j][ns] = jb.in[q].blocks;
-            w.seg_isws[j][ns] = jb.in[q].is_ws;
         }
         w.job_nseg[j] = ns;
         w.job_slab[j] = jb.slab_off;
         max_blk = jb.NBz + jb.KB > max_blk ? jb.NBz + jb.KB : max_blk;
     }
-    w.job_wg0[p.n_jobs] = wg;
     w.stage_bytes = max_blk * p.fpb * kFragBytes;
-    const size_t lds = 2 * static_cast<size_t>(w.stage_bytes);
+    // as many stages as fit in 160 KiB (+1 KB scratch): 4 for bf16, 2 for fp32
+    w.nstage = static_cast<int>((160 * 1024 - kFragBytes) / w.stage_bytes);
+    if (w.nstage > 4) w.nstage = 4;
+    const size_t lds = static_cast<size_t>(w.nstage) * w.stage_bytes + kFragBytes;
+    NR_REQUIRE(w.nstage >= 2, "nr_mlp_backward_dw: a %d-byte stage does not fit twice in LDS", w.stage_bytes);
     NR_REQUIRE(lds <= 160 * 1024, "nr_mlp_backward_dw: %zu bytes of LDS staging exceeds 160 KiB", lds);
+    const dim3 grid(static_cast<unsigned>(p.n_jobs * z.chunks)), block(kDwThreads);
     if (p.prec == NR_PREC_BF16)
-        hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_BF16>, dim3(wg), dim3(kThreads), lds, s, w);
+        hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_BF16>, grid, block, lds, s, w);
     else
-        hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_FP32>, dim3(wg), dim3(kThreads), lds, s, w);
+        hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_FP32>, grid, block, lds, s, w);
     NR_LAUNCH_CHECK("nr_mlp_backward_dw");
     return NR_OK;
 }
@@ -1420,19 +1467,18 @@ int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M, const void* worksp
     r.n_red = p.n_red;
     for (int k = 0; k < p.n_red; ++k) {
         const ReduceRange& rr = p.red[k];
-        r.red_row0[k] = rr.row0;
-        r.red_rows[k] = rr.rows;
-        r.red_in[k] = rr.in;
-        r.red_KB[k] = p.job[rr.job].KB;
-        r.red_w_off[k] = rr.w_off;
-        r.red_b_off[k] = rr.b_off;
-        r.red_slab[k] = p.job[rr.job].slab_off;
-        r.red_nseg[k] = rr.nseg;
-        for (int q = 0; q < rr.nseg; ++q) {
-            r.red_seg_col0[k][q] = rr.seg_col0[q];
-            r.red_seg_w[k][q] = rr.seg_w[q];
-            r.red_seg_blk0[k][q] = rr.seg_blk0[q];
-        }
+        r.rows[k] = rr.rows;
+        r.in[k] = rr.in;
+        r.nseg[k] = rr.nseg;
+        r.bjob[k] = rr.bjob;
+        r.brow0[k] = rr.brow0;
+        r.w_off[k] = rr.w_off;
+        r.b_off[k] = rr.b_off;
+        for (int q = 0; q < rr.nseg; ++q) r.seg[k][q] = rr.seg[q];
+    }
+    for (int j = 0; j < p.n_jobs; ++j) {
+        r.job_slab[j] = p.job[j].slab_off;
+        r.job_KB[j] = p.job[j].KB;
     }
     hipLaunchKernelGGL(mlp_dw_reduce_kernel, dim3(static_cast<unsigned>(ceil_div_ll(p.param_count, 256))), dim3(256),
                        0, s, r);

@@ -26,8 +26,10 @@ constexpr int kHB = kHidden / 32;      // hidden feature blocks
 constexpr int kMaxTrunk = 16;          // num_hidden_layers upper bound
 constexpr int kMaxMfmaLayers = kMaxTrunk + 2;  // trunk + feature + dir
 constexpr int kFragBytes = 1024;       // one wave-wide 16-B-per-lane operand fragment
-constexpr int kMaxJobs = kMaxTrunk + 3;  // dW jobs: trunk + (feat & sigma) + dir + rgb
+constexpr int kMaxJobs = kMaxTrunk + 8;  // dW jobs: x-jobs + trunk h-jobs + feat + heads + dir
 constexpr int kMaxSeg = 2;
+constexpr int kMaxJobSeg = 4;            // tensors on either side of a dW job
+constexpr int kMaxRed = kMaxTrunk + 4;    // reduce ranges: trunk, feat, sigma, rgb, dir
 
 // One input segment of a linear layer: columns [col0, col0+width) of W,
 // occupying ceil(width/32) consecutive 32-wide input blocks.
@@ -51,12 +53,13 @@ struct DwSeg {
     int is_ws, tensor, blocks;
 };
 
-// A dW job: gradients of the linear layers whose dz blocks are `dz` and whose
-// input blocks are `in`.  Output slab per chunk: (NBz*32) x (KB*32 + 1) floats,
-// the last column holding the bias partial.
+// A dW job: the products dz^T . in of every (dz tensor, input tensor) pair it
+// lists, for the tiles of one chunk: an NBz x KB grid of 32x32 blocks (at most
+// 64 blocks = 8 waves x 4x2).  Output slab per chunk: (NBz*32) x (KB*32 + 1)
+// floats, the last column holding the bias partial sums of the dz rows.
 struct DwJob {
     int ndz, nin;
-    DwSeg dz[kMaxSeg], in[kMaxSeg];
+    DwSeg dz[kMaxJobSeg], in[kMaxJobSeg];
     int NBz, KB;
     int64_t slab_off;  // float offset of this job's slab inside one chunk's slab set
 };
@@ -65,13 +68,18 @@ struct DwJob {
 enum SavedId { SV_XENC = 0, SV_H0 = 1 /* .. SV_H0+n_layers-1 */ };
 enum WsId { WS_DZ0 = 0 /* dz of trunk i: WS_DZ0+i; then feat, dir, heads */ };
 
-// Per-parameter-range map for the slab reduction: parameters [p0, p0+rows*in)
-// are W rows `row0..` of a job slab, and [b0, b0+rows) its bias column.
+// Per-parameter-range map for the slab reduction: W (rows x in, at w_off) takes
+// its column segments from job slabs (slab row slab_row0 + r, column
+// slab_col0 + c - col0); the bias (b_off, rows) from job bjob's bias column.
+struct RedSeg {
+    int col0, width, job, slab_row0, slab_col0;
+};
 struct ReduceRange {
-    int job, row0, rows, in;
+    int rows, in;
     int64_t w_off, b_off;
     int nseg;
-    int seg_col0[kMaxSeg], seg_w[kMaxSeg], seg_blk0[kMaxSeg];
+    RedSeg seg[kMaxSeg];
+    int bjob, brow0;
 };
 
 struct MlpPlan {
@@ -100,7 +108,7 @@ struct MlpPlan {
     DwJob job[kMaxJobs];
     int64_t slab_floats_per_chunk;
     int n_red;
-    ReduceRange red[kMaxJobs + 2];
+    ReduceRange red[kMaxRed];
 };
 
 inline bool is_skip(const MlpPlan& p, int i) { return (p.skips >> i) & 1u; }
