@@ -69,6 +69,15 @@ __device__ __forceinline__ void zero(f32x16& a) {
 #define NR_SIN sinf
 #define NR_COS cosf
 #endif
+// lane * 16 recomputed in place (2 VALU): lane-derived offsets are otherwise kept
+// live across the whole kernel, and under register pressure spilled and
+// reloaded with a vmcnt(0) that also drains the in-flight weight stream.
+__device__ __forceinline__ uint32_t lane16() {
+    uint32_t v;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 4, %0" : "=v"(v));
+    return v;
+}
+
 // Positional-encoding feature f of a 3-vector (model.py:72-80): [x | sin 2^0 x | cos 2^0 x | ...].
 __device__ __forceinline__ float pe_feat(float x0, float x1, float x2, int f, int L) {
     if (f < 3) return f == 0 ? x0 : (f == 1 ? x1 : x2);
@@ -112,8 +121,9 @@ __device__ __forceinline__ void pe_feat_bwd(float x0, float x1, float x2, int f,
 // One 32-feature block of a tile as a B-operand image: FPB fragments of 1 KB.
 template <int PREC>
 __device__ __forceinline__ void store_img(char* __restrict__ region, int64_t tile, int nblk, int blk,
-                                          const InBlk<PREC>& v, int lane) {
-    char* base = region + ((tile * nblk + blk) * kFPB<PREC>) * static_cast<int64_t>(kFragBytes) + lane * 16;
+                                          const InBlk<PREC>& v, int) {
+    // wave-uniform base (tile is per wave) + the lane's 16 B: saddr + voffset stores
+    char* base = region + ((tile * nblk + blk) * kFPB<PREC>) * static_cast<int64_t>(kFragBytes) + lane16();
     if constexpr (PREC == NR_PREC_BF16) {
         *reinterpret_cast<bf16x8*>(base) = v.s[0];
         *reinterpret_cast<bf16x8*>(base + kFragBytes) = v.s[1];
@@ -127,8 +137,8 @@ __device__ __forceinline__ void store_img(char* __restrict__ region, int64_t til
 
 template <int PREC>
 __device__ __forceinline__ void load_img(const char* __restrict__ region, int64_t tile, int nblk, int blk,
-                                         InBlk<PREC>& v, int lane) {
-    const char* base = region + ((tile * nblk + blk) * kFPB<PREC>) * static_cast<int64_t>(kFragBytes) + lane * 16;
+                                         InBlk<PREC>& v, int) {
+    const char* base = region + ((tile * nblk + blk) * kFPB<PREC>) * static_cast<int64_t>(kFragBytes) + lane16();
     if constexpr (PREC == NR_PREC_BF16) {
         v.s[0] = *reinterpret_cast<const bf16x8*>(base);
         v.s[1] = *reinterpret_cast<const bf16x8*>(base + kFragBytes);
@@ -144,18 +154,36 @@ __device__ __forceinline__ void load_img(const char* __restrict__ region, int64_
 
 // bias + optional ReLU on NBO blocks; mask bits (bit (nb&1)*16+r of word nb>>1) into w[4].
 // Vector images (mlp_plan.hpp): 16 fp32 per (block, lane half) in accumulator order.
-// The opaque lane-half copy keeps the compiler from hoisting these loads out of
-// the layer loops as invariants (they would then stay live, and spill).
-__device__ __forceinline__ const f32x4* vimg(const char* packed, int64_t off, int lane) {
-    int hl = lane >> 5;
-    asm volatile("" : "+v"(hl));
-    return reinterpret_cast<const f32x4*>(packed + off) + hl * 4;
+// Vector images (biases, w_sigma, W_rgb: 16 fp32 per (block, lane half)) are
+// read with SCALAR loads through the constant address space and selected per
+// lane half, so they cost no vector registers; the opaque pointer copy keeps the
+// loads from being hoisted out of the layer loops as invariants.
+typedef const __attribute__((address_space(4))) float cfloat;
+
+struct VImg {
+    cfloat* p;
+    bool hi;
+    // registers 4g..4g+3 of block nb, for this lane's half
+    __device__ __forceinline__ f32x4 g4(int nb, int g) const {
+        f32x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float lo = p[(2 * nb) * 16 + 4 * g + e], up = p[(2 * nb + 1) * 16 + 4 * g + e];
+            r[e] = hi ? up : lo;
+        }
+        return r;
+    }
+};
+
+__device__ __forceinline__ VImg vimg(const char* packed, int64_t off, int lane) {
+    const char* q = packed + off;
+    asm volatile("" : "+s"(q));
+    return VImg{(cfloat*)(q), (lane >> 5) != 0};
 }
-// f32x4 g (registers 4g..4g+3) of block nb
-#define NR_VEC(img, nb, g) ((img)[(nb) * 8 + (g)])
+#define NR_VEC(img, nb, g) ((img).g4((nb), (g)))
 
 template <int NBO, bool RELU>
-__device__ __forceinline__ void bias_act(f32x16 (&acc)[NBO], const f32x4* __restrict__ bias, unsigned (&w)[4]) {
+__device__ __forceinline__ void bias_act(f32x16 (&acc)[NBO], const VImg& bias, unsigned (&w)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) w[q] = 0u;
 #pragma unroll
@@ -197,7 +225,8 @@ constexpr int kMaxChunks = 176;  // >= sum of KB (forward) or NB (backward) over
 struct StreamDesc {
     int64_t base;                  // byte offset of the stream's first chunk in `packed`
     int nq;                        // chunks
-    int ckb[kMaxChunks];           // chunk sizes in KB
+    int ckb[kMaxChunks];           // bytes loaded per chunk, in KB
+    int cadv[kMaxChunks];          // bytes to the next chunk, in KB (>= ckb: a chunk may be loaded in part)
 };
 
 struct Ring {
@@ -205,10 +234,34 @@ struct Ring {
     int slot_bytes;
     int q;                         // chunk in the current slot
     const char* src;               // next chunk to load
+    int wv;                        // wave index in the workgroup (wave-uniform)
 };
 
+#ifndef NR_STAGE_GLDS
+#define NR_STAGE_GLDS 1
+#endif
 template <int G, int NT>
 struct Stager {
+#if NR_STAGE_GLDS
+    // LDS-DMA staging: chunk q goes straight into its slot (no registers); the
+    // barrier that publishes it is preceded by vmcnt(0).
+    __device__ __forceinline__ void load(Ring& ring, const StreamDesc& sd, int q, int tid) {
+        if (q >= sd.nq) return;
+        const int bytes = sd.ckb[q] * 1024;
+        char* slot = ring.lds + (q & 1) * ring.slot_bytes;
+        const uint32_t l16 = lane16();
+        for (int pc = ring.wv; pc * 1024 < bytes; pc += NT / 64)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(ring.src + pc * 1024 + l16),
+                (__attribute__((address_space(3))) void*)(slot + pc * 1024), 16, 0, 0);
+        ring.src += sd.cadv[q] * 1024;
+    }
+
+    __device__ __forceinline__ void store(char*, const StreamDesc&, int, int) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#else
+    // register staging: load(q) before chunk q-1's MFMAs, store after them
     u32x4 v[G];
 
     __device__ __forceinline__ void load(Ring& ring, const StreamDesc& sd, int q, int tid) {
@@ -219,7 +272,7 @@ struct Stager {
             const int b = (g * NT + tid) * 16;
             if (b < bytes) v[g] = *reinterpret_cast<const u32x4*>(ring.src + b);
         }
-        ring.src += bytes;
+        ring.src += sd.cadv[q] * 1024;
     }
 
     __device__ __forceinline__ void store(char* slot, const StreamDesc& sd, int q, int tid) {
@@ -231,21 +284,51 @@ struct Stager {
             if (b < bytes) *reinterpret_cast<u32x4*>(slot + b) = v[g];
         }
     }
+#endif
+};
+
+// Per-wave activation storage of NBLK 32-feature blocks for TPW tiles: in
+// registers, or (bf16) in the wave's own LDS region as B-operand images (frees
+// the 64 registers that let two waves share a SIMD without spilling).
+template <int PREC, int TPW, int NBLK, bool LDS>
+struct Act {
+    InBlk<PREC> v[TPW][NBLK];
+    __device__ __forceinline__ InBlk<PREC> operator()(int t, int kb) const { return v[t][kb]; }
+    __device__ __forceinline__ void put(int t, int nb, const InBlk<PREC>& x) { v[t][nb] = x; }
+};
+template <int TPW, int NBLK>
+struct Act<NR_PREC_BF16, TPW, NBLK, true> {
+    char* base;  // the wave's region (wave-uniform)
+    static constexpr int kBytes = TPW * NBLK * 2 * kFragBytes;
+    __device__ __forceinline__ InBlk<NR_PREC_BF16> operator()(int t, int kb) const {
+        const char* p = base + lane16() + (t * NBLK + kb) * 2 * kFragBytes;
+        InBlk<NR_PREC_BF16> r;
+        r.s[0] = *reinterpret_cast<const bf16x8*>(p);
+        r.s[1] = *reinterpret_cast<const bf16x8*>(p + kFragBytes);
+        return r;
+    }
+    __device__ __forceinline__ void put(int t, int nb, const InBlk<NR_PREC_BF16>& x) {
+        char* p = base + lane16() + (t * NBLK + nb) * 2 * kFragBytes;
+        *reinterpret_cast<bf16x8*>(p) = x.s[0];
+        *reinterpret_cast<bf16x8*>(p + kFragBytes) = x.s[1];
+    }
 };
 
 // acc1[t][r] += A(row block nb0 + r) . in[t]   (r < N1)
 // acc2[t][r] += A(row block nb0 + N1 + r) . in[t]   (r < N2)
 // over KBN consecutive stream chunks (k blocks).
-template <int PREC, int TPW, int N1, int N2, int KBN, int G, int NT>
+template <int PREC, int TPW, int N1, int N2, int KBN, int G, int NT, class Src>
 __device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1],
-                                            f32x16 (&acc2)[TPW][N2 > 0 ? N2 : 1], int nb0,
-                                            const InBlk<PREC> (&in)[TPW][KBN], Ring& ring, Stager<G, NT>& st,
-                                            const char* __restrict__ packed, const StreamDesc& sd, int tid,
-                                            int lane) {
+                                            f32x16 (&acc2)[TPW][N2 > 0 ? N2 : 1], int nb0, const Src& src,
+                                            Ring& ring, Stager<G, NT>& st, const char* __restrict__ packed,
+                                            const StreamDesc& sd, int tid, int lane) {
 #pragma unroll
     for (int kb = 0; kb < KBN; ++kb) {
         st.load(ring, sd, ring.q + 1, tid);
-        const char* slot = ring.lds + (ring.q & 1) * ring.slot_bytes + lane * 16;
+        const char* slot = ring.lds + (ring.q & 1) * ring.slot_bytes + lane16();
+        InBlk<PREC> in[TPW];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) in[t] = src(t, kb);
 #pragma unroll
         for (int r = 0; r < N1 + N2; ++r) {
             const char* fp = slot + (nb0 + r) * kFPB<PREC> * kFragBytes;
@@ -260,11 +343,11 @@ __device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1]
 #pragma unroll
                 for (int t = 0; t < TPW; ++t) {
                     if (r < N1) {
-                        acc1[t][r1] = mfma_bf16(a0, in[t][kb].s[0], acc1[t][r1]);
-                        acc1[t][r1] = mfma_bf16(a1, in[t][kb].s[1], acc1[t][r1]);
+                        acc1[t][r1] = mfma_bf16(a0, in[t].s[0], acc1[t][r1]);
+                        acc1[t][r1] = mfma_bf16(a1, in[t].s[1], acc1[t][r1]);
                     } else {
-                        acc2[t][r2] = mfma_bf16(a0, in[t][kb].s[0], acc2[t][r2]);
-                        acc2[t][r2] = mfma_bf16(a1, in[t][kb].s[1], acc2[t][r2]);
+                        acc2[t][r2] = mfma_bf16(a0, in[t].s[0], acc2[t][r2]);
+                        acc2[t][r2] = mfma_bf16(a1, in[t].s[1], acc2[t][r2]);
                     }
                 }
             } else {
@@ -276,9 +359,9 @@ __device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1]
 #pragma unroll
                         for (int t = 0; t < TPW; ++t) {
                             if (r < N1)
-                                acc1[t][r1] = mfma_f32(a[e], in[t][kb].v[4 * tq + e], acc1[t][r1]);
+                                acc1[t][r1] = mfma_f32(a[e], in[t].v[4 * tq + e], acc1[t][r1]);
                             else
-                                acc2[t][r2] = mfma_f32(a[e], in[t][kb].v[4 * tq + e], acc2[t][r2]);
+                                acc2[t][r2] = mfma_f32(a[e], in[t].v[4 * tq + e], acc2[t][r2]);
                         }
                 }
             }
@@ -325,7 +408,8 @@ template <int PREC, int XB, int DB, bool TRAIN, int TPW, int G, int NT>
 __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ml = lane & 31;
-    const int64_t tile0 = (static_cast<int64_t>(blockIdx.x) * (NT / 64) + (tid >> 6)) * TPW;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t tile0 = (static_cast<int64_t>(blockIdx.x) * (NT / 64) + wv) * TPW;
     const int n = a.n_layers;
     float px[TPW][3];
     bool tok[TPW];
@@ -340,12 +424,15 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     }
     u32x4* masks = reinterpret_cast<u32x4*>(a.saved + a.mask_off);
 
-    Ring ring{lds, a.slot_bytes, 0, nullptr};
+    Ring ring{lds, a.slot_bytes, 0, nullptr, wv};
     Stager<G, NT> st;
     stream_begin(ring, st, a.packed, a.sd, tid);
 
     f32x16 acc[TPW][kHB];
-    InBlk<PREC> hin[TPW][kHB];
+    constexpr bool ACT_LDS = PREC == NR_PREC_BF16 && NT == 512;
+    Act<PREC, TPW, kHB, ACT_LDS> hin;
+    if constexpr (ACT_LDS)
+        hin.base = lds + 2 * a.slot_bytes + wv * Act<PREC, TPW, kHB, ACT_LDS>::kBytes;
     f32x16 dummy[TPW][1];
     unsigned w[4];
     for (int i = 0; i < n; ++i) {
@@ -357,16 +444,16 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
         if (i == 0 || skip_in) {
             // x_enc is not kept in registers: the skip layer reloads the saved
             // copy (training) or recomputes it (inference)
-            InBlk<PREC> xe[TPW][XB];
+            Act<PREC, TPW, XB, false> xe;
 #pragma unroll
             for (int t = 0; t < TPW; ++t) {
                 if (TRAIN && i > 0) {
 #pragma unroll
                     for (int kb = 0; kb < XB; ++kb) {
                         if (tok[t])
-                            load_img<PREC>(a.saved + a.sv_off[SV_XENC], tile0 + t, XB, kb, xe[t][kb], lane);
+                            load_img<PREC>(a.saved + a.sv_off[SV_XENC], tile0 + t, XB, kb, xe.v[t][kb], lane);
                         else
-                            xe[t][kb] = InBlk<PREC>{};
+                            xe.v[t][kb] = InBlk<PREC>{};
                     }
                     continue;
                 }
@@ -379,9 +466,9 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                     f32x16 v;
 #pragma unroll
                     for (int r = 0; r < 16; ++r) v[r] = pe_feat(p0, p1, p2, 32 * kb + acc_row(r, h), a.L);
-                    to_in<PREC>(v, xe[t][kb]);
+                    to_in<PREC>(v, xe.v[t][kb]);
                     if constexpr (TRAIN)
-                        if (tok[t]) store_img<PREC>(a.saved + a.sv_off[SV_XENC], tile0 + t, XB, kb, xe[t][kb], lane);
+                        if (tok[t]) store_img<PREC>(a.saved + a.sv_off[SV_XENC], tile0 + t, XB, kb, xe.v[t][kb], lane);
                 }
             }
             stream_gemm<PREC, TPW, kHB, 0, XB, G, NT>(acc, dummy, 0, xe, ring, st, a.packed, a.sd, tid, lane);
@@ -391,22 +478,22 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
         for (int t = 0; t < TPW; ++t) {
             bias_act<kHB, true>(acc[t], vimg(a.packed, a.vb[i], lane), w);
 #pragma unroll
-            for (int nb = 0; nb < kHB; ++nb) to_in<PREC>(acc[t][nb], hin[t][nb]);
-            if constexpr (TRAIN) {
-                if (tok[t]) {
-#pragma unroll
-                    for (int nb = 0; nb < kHB; ++nb)
-                        store_img<PREC>(a.saved + a.sv_off[SV_H0 + i], tile0 + t, kHB, nb, hin[t][nb], lane);
-                    masks[((tile0 + t) * a.n_mask + i) * 64 + lane] = u32x4{w[0], w[1], w[2], w[3]};
-                }
+            for (int nb = 0; nb < kHB; ++nb) {
+                InBlk<PREC> v;
+                to_in<PREC>(acc[t][nb], v);
+                hin.put(t, nb, v);
+                if constexpr (TRAIN)
+                    if (tok[t]) store_img<PREC>(a.saved + a.sv_off[SV_H0 + i], tile0 + t, kHB, nb, v, lane);
             }
+            if constexpr (TRAIN)
+                if (tok[t]) masks[((tile0 + t) * a.n_mask + i) * 64 + lane] = u32x4{w[0], w[1], w[2], w[3]};
         }
     }
 
     // sigma head (VALU): relu(w_sigma . h + b), from the fp32 activations
     float sp[TPW];
     {
-        const f32x4* ws = vimg(a.packed, a.vsig, lane);
+        const VImg ws = vimg(a.packed, a.vsig, lane);
 #pragma unroll
         for (int t = 0; t < TPW; ++t) sp[t] = 0.f;
 #pragma unroll
@@ -438,9 +525,11 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
         bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[n], lane), w);
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb) {
-            to_in<PREC>(acc[t][nb], hin[t][nb]);
+            InBlk<PREC> v;
+            to_in<PREC>(acc[t][nb], v);
+            hin.put(t, nb, v);
             if constexpr (TRAIN)
-                if (tok[t]) store_img<PREC>(a.saved + a.sv_off[a.sv_feat], tile0 + t, kHB, nb, hin[t][nb], lane);
+                if (tok[t]) store_img<PREC>(a.saved + a.sv_off[a.sv_feat], tile0 + t, kHB, nb, v, lane);
         }
     }
 
@@ -453,7 +542,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
         for (int nb = 0; nb < NC; ++nb) zero(ac[t][nb]);
     stream_gemm<PREC, TPW, NC, 0, kHB, G, NT>(ac, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane);
     if constexpr (DB > 0) {
-        InBlk<PREC> de[TPW][DB];
+        Act<PREC, TPW, DB, false> de;
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
             const int64_t m = (tile0 + t) * 32 + ml;
@@ -465,9 +554,9 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                 f32x16 v;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) v[r] = pe_feat(d0, d1, d2, 32 * kb + acc_row(r, h), a.Ld);
-                to_in<PREC>(v, de[t][kb]);
+                to_in<PREC>(v, de.v[t][kb]);
                 if constexpr (TRAIN)
-                    if (tok[t]) store_img<PREC>(a.saved + a.sv_off[a.sv_denc], tile0 + t, DB, kb, de[t][kb], lane);
+                    if (tok[t]) store_img<PREC>(a.saved + a.sv_off[a.sv_denc], tile0 + t, DB, kb, de.v[t][kb], lane);
             }
         }
         stream_gemm<PREC, TPW, NC, 0, DB, G, NT>(ac, dummy, 0, de, ring, st, a.packed, a.sd, tid, lane);
@@ -490,7 +579,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
         float pr[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const f32x4* wr = vimg(a.packed, a.vrgb, lane) + c * NC * 8;
+            const VImg wr = vimg(a.packed, a.vrgb + c * NC * 128, lane);
             float s = 0.f;
 #pragma unroll
             for (int nb = 0; nb < NC; ++nb)
@@ -544,7 +633,8 @@ template <int PREC, int XB, int DB, int TPW, int G, int NT, bool WANT_X>
 __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ml = lane & 31;
-    const int64_t tile0 = (static_cast<int64_t>(blockIdx.x) * (NT / 64) + (tid >> 6)) * TPW;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t tile0 = (static_cast<int64_t>(blockIdx.x) * (NT / 64) + wv) * TPW;
     const int n = a.n_layers;
     const u32x4* masks = reinterpret_cast<const u32x4*>(a.saved + a.mask_off);
     bool tok[TPW];
@@ -554,14 +644,14 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
         return tok[t] ? masks[((tile0 + t) * a.n_mask + layer) * 64 + lane] : u32x4{0u, 0u, 0u, 0u};
     };
 
-    Ring ring{lds, a.slot_bytes, 0, nullptr};
+    Ring ring{lds, a.slot_bytes, 0, nullptr, wv};
     Stager<G, NT> st;
     stream_begin(ring, st, a.packed, a.sd, tid);
 
     // heads: sigmoid / relu backward (torch: g * (1 - y) * y ; g * (y > 0))
     constexpr int NC = kHB / 2;
     float dzs[TPW];
-    InBlk<PREC> cin[TPW][NC];
+    Act<PREC, TPW, NC, false> cin;
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
         const int64_t m = (tile0 + t) * 32 + ml;
@@ -592,26 +682,29 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
         }
         // dz_c = (W_rgb^T dz_rgb) * [h_c > 0]
         f32x16 dc[NC];
-        const f32x4* wr = vimg(a.packed, a.vrgb, lane);
+        const VImg wr = vimg(a.packed, a.vrgb, lane);
 #pragma unroll
         for (int nb = 0; nb < NC; ++nb)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const f32x4 w0 = NR_VEC(wr, nb, g), w1 = NR_VEC(wr + NC * 8, nb, g), w2 = NR_VEC(wr + 2 * NC * 8, nb, g);
+                const f32x4 w0 = NR_VEC(wr, nb, g), w1 = NR_VEC(wr, NC + nb, g), w2 = NR_VEC(wr, 2 * NC + nb, g);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) dc[nb][4 * g + e] = (w0[e] * dr[0] + w1[e] * dr[1]) + w2[e] * dr[2];
             }
         apply_mask<NC>(dc, mask_of(t, n));
 #pragma unroll
         for (int nb = 0; nb < NC; ++nb) {
-            to_in<PREC>(dc[nb], cin[t][nb]);
-            if (tok[t]) store_img<PREC>(a.ws + a.ws_off[a.ws_dir], tile0 + t, NC, nb, cin[t][nb], lane);
+            to_in<PREC>(dc[nb], cin.v[t][nb]);
+            if (tok[t]) store_img<PREC>(a.ws + a.ws_off[a.ws_dir], tile0 + t, NC, nb, cin.v[t][nb], lane);
         }
     }
 
     // d [feat | d_enc] = W_dir^T dz_c   (feature_linear has no activation: dz_feat = d feat)
     f32x16 acc[TPW][kHB];
-    InBlk<PREC> hin[TPW][kHB];
+    constexpr bool ACT_LDS = PREC == NR_PREC_BF16 && NT == 512;
+    Act<PREC, TPW, kHB, ACT_LDS> hin;
+    if constexpr (ACT_LDS)
+        hin.base = lds + 2 * a.slot_bytes + wv * Act<PREC, TPW, kHB, ACT_LDS>::kBytes;
 #pragma unroll
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
@@ -652,8 +745,10 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb) {
-            to_in<PREC>(acc[t][nb], hin[t][nb]);
-            if (tok[t]) store_img<PREC>(a.ws + a.ws_off[a.ws_feat], tile0 + t, kHB, nb, hin[t][nb], lane);
+            InBlk<PREC> v;
+            to_in<PREC>(acc[t][nb], v);
+            hin.put(t, nb, v);
+            if (tok[t]) store_img<PREC>(a.ws + a.ws_off[a.ws_feat], tile0 + t, kHB, nb, v, lane);
         }
 
     // d h_{n-1} = W_feat^T dz_feat + w_sigma dz_sigma, then * [h_{n-1} > 0]
@@ -664,7 +759,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
         for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
     stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane);
     {
-        const f32x4* ws = vimg(a.packed, a.vsig, lane);
+        const VImg ws = vimg(a.packed, a.vsig, lane);
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb)
 #pragma unroll
@@ -681,8 +776,10 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
         apply_mask<kHB>(acc[t], mask_of(t, n - 1));
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb) {
-            to_in<PREC>(acc[t][nb], hin[t][nb]);
-            if (tok[t]) store_img<PREC>(a.ws + a.ws_off[WS_DZ0 + n - 1], tile0 + t, kHB, nb, hin[t][nb], lane);
+            InBlk<PREC> v;
+            to_in<PREC>(acc[t][nb], v);
+            hin.put(t, nb, v);
+            if (tok[t]) store_img<PREC>(a.ws + a.ws_off[WS_DZ0 + n - 1], tile0 + t, kHB, nb, v, lane);
         }
     }
 
@@ -699,10 +796,12 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
         if ((a.skips >> (i - 1)) & 1u) {
+            // W^T row blocks of a skip layer are [h (8) | x_enc (XB)]; without g_x
+            // only the h rows are streamed
             if constexpr (XBX > 0)
-                stream_gemm<PREC, TPW, XBX, kHB, kHB, G, NT>(dxe, acc, 0, hin, ring, st, a.packed, a.sd, tid, lane);
+                stream_gemm<PREC, TPW, kHB, XBX, kHB, G, NT>(acc, dxe, 0, hin, ring, st, a.packed, a.sd, tid, lane);
             else
-                stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, XB, hin, ring, st, a.packed, a.sd, tid, lane);
+                stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane);
         } else {
             stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane);
         }
@@ -711,8 +810,10 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
             apply_mask<kHB>(acc[t], mask_of(t, i - 1));
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) {
-                to_in<PREC>(acc[t][nb], hin[t][nb]);
-                if (tok[t]) store_img<PREC>(a.ws + a.ws_off[WS_DZ0 + i - 1], tile0 + t, kHB, nb, hin[t][nb], lane);
+                InBlk<PREC> v;
+                to_in<PREC>(acc[t][nb], v);
+                hin.put(t, nb, v);
+                if (tok[t]) store_img<PREC>(a.ws + a.ws_off[WS_DZ0 + i - 1], tile0 + t, kHB, nb, v, lane);
             }
         }
     }
@@ -1040,6 +1141,7 @@ struct PackArgs {
     int in[kMaxMfmaLayers], NB[kMaxMfmaLayers], KB[kMaxMfmaLayers], nseg[kMaxMfmaLayers];
     int seg_col0[kMaxMfmaLayers][kMaxSeg], seg_w[kMaxMfmaLayers][kMaxSeg], seg_blk[kMaxMfmaLayers][kMaxSeg];
     int64_t pk[kMaxMfmaLayers], pkb[kMaxMfmaLayers];
+    int bwd_rot[kMaxMfmaLayers];  // W^T row-block rotation: skip layers put the h rows first
     int64_t cum[kMaxMfmaLayers + 1];
 };
 
@@ -1080,7 +1182,8 @@ __global__ void mlp_pack_kernel(PackArgs a) {
         row = 32 * nb + i;
         col = pack_col(a, l, kb, kk);
     } else {  // W^T: A[i][k] = W[32ob + k][col(ib, i)], chunk ob, row block ib
-        const int ob = static_cast<int>(blk / a.KB[l]), ib = static_cast<int>(blk % a.KB[l]);
+        const int ob = static_cast<int>(blk / a.KB[l]);
+        const int ib = static_cast<int>((blk % a.KB[l] + a.bwd_rot[l]) % a.KB[l]);
         row = 32 * ob + kk;
         col = pack_col(a, l, ib, i);
     }
@@ -1135,15 +1238,18 @@ bool plan_or_error(const NrMlpConfig* cfg, MlpPlan* p) {
 // forward (training) 3.25 ms at 256 vs 4.09 ms at 512 (the 512 build spills);
 // backward dX 2.12 ms at 256 vs 1.70 ms at 512.
 #ifndef NR_FWD_NT
-#define NR_FWD_NT 256
+#define NR_FWD_NT 512
 #endif
 #ifndef NR_BWD_NT
 #define NR_BWD_NT 512
 #endif
 #define NR_FWD_TPW 1
 
-void add_stream_layer(StreamDesc& sd, int nchunks, int chunk_kb) {
-    for (int c = 0; c < nchunks && sd.nq < kMaxChunks; ++c) sd.ckb[sd.nq++] = chunk_kb;
+void add_stream_layer(StreamDesc& sd, int nchunks, int chunk_kb, int load_kb = -1) {
+    for (int c = 0; c < nchunks && sd.nq < kMaxChunks; ++c) {
+        sd.ckb[sd.nq] = load_kb < 0 ? chunk_kb : load_kb;
+        sd.cadv[sd.nq++] = chunk_kb;
+    }
 }
 
 int max_chunk(const StreamDesc& sd) {
@@ -1162,7 +1268,12 @@ int launch_fwd(const MlpPlan& p, FwdArgs& a, hipStream_t s) {
         return NR_EARG;
     }
     a.slot_bytes = mc;
-    const size_t lds = 2 * static_cast<size_t>(mc);
+    constexpr bool ACT_LDS = PREC == NR_PREC_BF16 && NT == 512;
+    const size_t lds = 2 * static_cast<size_t>(mc) + (ACT_LDS ? (NT / 64) * TPW * kHB * 2 * kFragBytes : 0);
+    if (lds > 160 * 1024) {
+        set_error("nr_mlp_forward: %zu bytes of LDS exceed 160 KiB", lds);
+        return NR_EARG;
+    }
     const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, (NT / 64) * TPW))), block(NT);
 #define NR_FWD(XB_, DB_)                                                                                 \
     if (p.XB == XB_ && p.DB == DB_) {                                                                    \
@@ -1192,7 +1303,12 @@ int launch_bwd(const MlpPlan& p, BwdArgs& a, hipStream_t s) {
         return NR_EARG;
     }
     a.slot_bytes = mc;
-    const size_t lds = 2 * static_cast<size_t>(mc);
+    constexpr bool ACT_LDS = PREC == NR_PREC_BF16 && NT == 512;
+    const size_t lds = 2 * static_cast<size_t>(mc) + (ACT_LDS ? (NT / 64) * TPW * kHB * 2 * kFragBytes : 0);
+    if (lds > 160 * 1024) {
+        set_error("nr_mlp_backward_dx: %zu bytes of LDS exceed 160 KiB", lds);
+        return NR_EARG;
+    }
     const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, (NT / 64) * TPW))), block(NT);
 #define NR_BWD(XB_, DB_)                                                                              \
     if (p.XB == XB_ && p.DB == DB_) {                                                                 \
@@ -1262,6 +1378,7 @@ int nr_mlp_pack(const NrMlpConfig* cfg, const float* params, void* packed, nr_st
         }
         a.pk[l] = d.pk_fwd;
         a.pkb[l] = d.pk_bwd;
+        a.bwd_rot[l] = (l > 0 && l < p.n_layers && is_skip(p, l - 1)) ? d.seg[0].blocks : 0;
         const int64_t elems = static_cast<int64_t>(d.NB) * d.KB * 1024;  // 32x32 elements per block
         a.cum[l + 1] = a.cum[l] + 2 * elems;
     }
@@ -1371,7 +1488,12 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     b.skips = p.skips;
     const int n = p.n_layers;
     const bool wx = g_x != nullptr || g_d != nullptr;
-    auto add_T = [&](int l) { add_stream_layer(b.sd, p.lin[l].NB, p.lin[l].KB * p.fpb); };
+    // a skip layer's W^T chunk is [h rows | x_enc rows] and dir's is [feat rows |
+    // d_enc rows]: without g_x / g_d only the first 8 row blocks are loaded
+    auto add_T = [&](int l) {
+        const bool partial = !wx && ((l > 0 && l < n && is_skip(p, l - 1)) || l == n + 1);
+        add_stream_layer(b.sd, p.lin[l].NB, p.lin[l].KB * p.fpb, partial ? kHB * p.fpb : -1);
+    };
     b.sd.base = p.lin[n + 1].pk_bwd;
     add_T(n + 1);  // dir^T
     add_T(n);      // feat^T
