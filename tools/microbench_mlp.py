@@ -5,7 +5,7 @@ from noisy_src import _hip
 from noisy_src.config import ModelConfig
 from noisy_src.model import NeRF
 MACS = 593408
-def bench(prec, M, reps=10):
+def bench(prec, M, reps=int(__import__("os").environ.get("MB_REPS", "20"))):
     torch.manual_seed(0)
     net = NeRF(ModelConfig(precision=prec)).cuda()
     net._ensure_flat(); packed = net._packed_for_forward(); flat = net._flat
