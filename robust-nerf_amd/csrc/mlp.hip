@@ -901,6 +901,9 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
 // dz and input blocks are staged into LDS by LDS-DMA (double buffered, 1-KB wave
 // pieces) and the sample-major MFMA operands are rebuilt from the B-operand
 // images.  Output slab per chunk: [dz row][input col | bias] fp32.
+#ifndef NR_DW_NSTAGE
+#define NR_DW_NSTAGE 4  // LDS staging ring depth of the dW kernel (tiles)
+#endif
 constexpr int kDwThreads = 512;
 constexpr int kDwWaves = kDwThreads / 64;
 constexpr int kDwP = 4, kDwQ = 2;  // blocks per wave: dz rows x input cols
@@ -977,23 +980,46 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     // Stage tile t into buffer b (the job's blocks, dz segments first).  Every wave
     // issues exactly `per_wave` 1-KB LDS-DMA pieces per tile (padding pieces re-load
     // piece 0 into a scratch KB), so a counted vmcnt can retire one stage while the
-    // next NS-2 stay in flight across the barrier.
+    // next NS-2 stay in flight across the barrier.  Each piece's per-lane source
+    // address, per-tile stride and LDS offset are resolved once per workgroup: the
+    // per-tile staging is one pointer bump and one DMA per piece (the segment walk
+    // per piece and tile made this kernel SALU-bound).
     const int total = (NBz + KB) * FPB;
     const int per_wave = (total + kDwWaves - 1) / kDwWaves;
-    auto stage = [&](int64_t t, int b) {
-        char* dst = lds + b * a.stage_bytes;
-        for (int k = 0; k < per_wave; ++k) {
+    constexpr int kMaxPW = PREC == NR_PREC_BF16 ? 6 : 10;
+    const char* psrc[kMaxPW];
+    int64_t pstride[kMaxPW];
+    int pdst[kMaxPW];  // LDS offset within a stage, or -1: scratch KB
+#pragma unroll
+    for (int k = 0; k < kMaxPW; ++k) {
+        psrc[k] = nullptr;
+        pstride[k] = 0;
+        pdst[k] = -1;
+        if (k < per_wave) {
             int pc = wv + k * kDwWaves;
-            char* d = lds + a.nstage * a.stage_bytes;  // scratch KB for padding pieces
-            if (pc >= total) pc = 0;
-            else d = dst + pc * kFragBytes;
+            const bool pad = pc >= total;
+            if (pad) pc = 0;
             int sg = 0, p0 = 0;
             while (pc >= p0 + a.seg_blocks[j][sg] * FPB) p0 += a.seg_blocks[j][sg++] * FPB;
             const int nb = a.seg_blocks[j][sg];
-            const char* src = a.seg_ptr[j][sg] + t * nb * BLK + (pc - p0) * kFragBytes;
             const int L = PREC == NR_PREC_BF16 ? dw_slot(lane, (pc - p0) % FPB) : lane;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + L * 16),
-                                             (__attribute__((address_space(3))) void*)(d), 16, 0, 0);
+            pstride[k] = static_cast<int64_t>(nb) * BLK;
+            psrc[k] = a.seg_ptr[j][sg] + t0 * pstride[k] + (pc - p0) * kFragBytes + L * 16;
+            pdst[k] = pad ? -1 : pc * kFragBytes;
+        }
+    }
+    // stages are issued in tile order, so each piece's source pointer just advances
+    auto stage = [&](int b) {
+        char* dst = lds + b * a.stage_bytes;
+        char* scratch = lds + a.nstage * a.stage_bytes;
+#pragma unroll
+        for (int k = 0; k < kMaxPW; ++k) {
+            if (k < per_wave) {
+                char* d = pdst[k] < 0 ? scratch : dst + pdst[k];
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(psrc[k]),
+                                                 (__attribute__((address_space(3))) void*)(d), 16, 0, 0);
+                psrc[k] += pstride[k];
+            }
         }
     };
     // wait until at most n of this wave's pieces are outstanding (n: wave-uniform)
@@ -1012,7 +1038,13 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     for (int p = 0; p < kDwP; ++p)
 #pragma unroll
         for (int q = 0; q < kDwQ; ++q) zero(acc[p][q]);
-    float bsum[kDwP] = {0.f, 0.f, 0.f, 0.f};
+    float bsum[kDwP] = {0.f, 0.f, 0.f, 0.f};  // fp32 images
+    f32x16 accb[kDwP];                        // bf16 images: D[row][*] = sum of dz[row]
+    bf16x8 ones;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = static_cast<__bf16>(1.0f);
+#pragma unroll
+    for (int p = 0; p < kDwP; ++p) zero(accb[p]);
     bool nval[kDwP], kval[kDwQ];
 #pragma unroll
     for (int p = 0; p < kDwP; ++p) nval[p] = active && kDwP * nbg + p < NBz;
@@ -1028,7 +1060,8 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
 
     const int NS = a.nstage;
     for (int k = 0; k < NS - 1; ++k)
-        if (t0 + k < t1) stage(t0 + k, k);
+        if (t0 + k < t1) stage(k);
+    int bcur = 0, bnext = NS - 1;  // stage of tile t, stage tile t+NS-1 goes to
     for (int64_t t = t0; t < t1; ++t) {
         // stages t+1 .. t+NS-2 may stay in flight
         int64_t ahead = t1 - 1 - t;
@@ -1036,9 +1069,11 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
         wait_pieces(per_wave * static_cast<int>(ahead));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (t + NS - 1 < t1) stage(t + NS - 1, static_cast<int>((t + NS - 1 - t0) % NS));
-        const char* buf = lds + static_cast<int>((t - t0) % NS) * a.stage_bytes;
-        if (active) {
+        if (t + NS - 1 < t1) stage(bnext);
+        bnext = bnext + 1 == NS ? 0 : bnext + 1;
+        const char* buf = lds + bcur * a.stage_bytes;
+        bcur = bcur + 1 == NS ? 0 : bcur + 1;
+        if (PREC == NR_PREC_BF16 || active) {
             if constexpr (PREC == NR_PREC_BF16) {
                 const uint32_t bufA = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf)) + kDwP * nbg * BLK;
                 const uint32_t bufB = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf)) +
@@ -1066,15 +1101,16 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
 #pragma unroll
                     for (int q = 0; q < kDwQ; ++q) Bm[q] = tr_pair(rb[q][0], rb[q][1]);
 #pragma unroll
-                    for (int p = 0; p < kDwP; ++p) {
-                        if (!nval[p]) continue;
-                        if (do_bias)
+                    // branch-free: blocks outside the job (and idle waves) accumulate
+                    // garbage that is never written (LDS reads past the image are in range
+                    // or return 0); per-MFMA validity branches made this loop SALU-bound
+                    for (int p = 0; p < kDwP; ++p)
 #pragma unroll
-                            for (int e = 0; e < 8; ++e) bsum[p] += static_cast<float>(A[p][e]);
+                        for (int q = 0; q < kDwQ; ++q) acc[p][q] = mfma_bf16(A[p], Bm[q], acc[p][q]);
+                    // bias gradient = dz summed over samples: an MFMA against ones
+                    if (do_bias)
 #pragma unroll
-                        for (int q = 0; q < kDwQ; ++q)
-                            if (kval[q]) acc[p][q] = mfma_bf16(A[p], Bm[q], acc[p][q]);
-                    }
+                        for (int p = 0; p < kDwP; ++p) accb[p] = mfma_bf16(A[p], ones, accb[p]);
                 }
             } else {
                 // fp32 image [tq][L][4]: operand row r <-> (hh = r>>4, reg i = r&15 -> frag i>>2, elem i&3)
@@ -1124,8 +1160,17 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
             }
         }
         if (do_bias) {
-            const float tot = bsum[p] + __shfl_xor(bsum[p], 32);
-            if (hl == 0) slab[static_cast<int64_t>(32 * (kDwP * nbg + p) + dw_feat(ml)) * ld + KB * 32] = tot;
+            if constexpr (PREC == NR_PREC_BF16) {
+                // every column of accb holds the row sums: lanes 0 and 32 (column 0) write them
+                if (ml == 0)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        slab[static_cast<int64_t>(32 * (kDwP * nbg + p) + dw_feat(acc_row(r, hl))) * ld + KB * 32] =
+                            accb[p][r];
+            } else {
+                const float tot = bsum[p] + __shfl_xor(bsum[p], 32);
+                if (hl == 0) slab[static_cast<int64_t>(32 * (kDwP * nbg + p) + dw_feat(ml)) * ld + KB * 32] = tot;
+            }
         }
     }
 }
@@ -1605,7 +1650,7 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
     w.stage_bytes = max_blk * p.fpb * kFragBytes;
     // as many stages as fit in 160 KiB (+1 KB scratch): 4 for bf16, 2 for fp32
     w.nstage = static_cast<int>((160 * 1024 - kFragBytes) / w.stage_bytes);
-    if (w.nstage > 4) w.nstage = 4;
+    if (w.nstage > NR_DW_NSTAGE) w.nstage = NR_DW_NSTAGE;
     const size_t lds = static_cast<size_t>(w.nstage) * w.stage_bytes + kFragBytes;
     NR_REQUIRE(w.nstage >= 2, "nr_mlp_backward_dw: a %d-byte stage does not fit twice in LDS", w.stage_bytes);
     NR_REQUIRE(lds <= 160 * 1024, "nr_mlp_backward_dw: %zu bytes of LDS staging exceeds 160 KiB", lds);

@@ -119,6 +119,7 @@ bool make_plan(const NrMlpConfig* cfg, MlpPlan* p, const char** why);
 // Byte sizes / offsets that depend on the number of samples.
 struct MlpSizes {
     int64_t tiles;
+    int64_t tiles_alloc;  // tiles rounded up to whole 16-tile groups: every fwd/bwd wave may store its tile
     int64_t saved_off[kMaxTrunk + 4];  // bytes
     int64_t mask_off;                  // bytes
     int64_t saved_bytes;
