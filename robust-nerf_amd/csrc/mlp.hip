@@ -47,14 +47,28 @@ struct InBlk<NR_PREC_FP32> {
 template <int PREC>
 constexpr int kFPB = PREC == NR_PREC_BF16 ? 2 : 4;  // 1-KB fragments per 32x32 block
 
+// Two fp32 -> one word of two bf16 (RNE), low half = lo: one v_cvt_pk_bf16_f32
+// (element-wise casts compile to one convert per element plus a v_perm per pair;
+// not inline asm: the hazard recognizer does not see an asm def that an MFMA reads).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned cvt_pk_bf16(float lo, float hi) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
+}
+
+// registers 8 hf .. 8 hf + 7 of an accumulator as a bf16x8 operand
+__device__ __forceinline__ bf16x8 pack8(const f32x16& a, int hf) {
+    u32x4 w;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) w[m] = cvt_pk_bf16(a[8 * hf + 2 * m], a[8 * hf + 2 * m + 1]);
+    return __builtin_bit_cast(bf16x8, w);
+}
+
 template <int PREC>
 __device__ __forceinline__ void to_in(const f32x16& a, InBlk<PREC>& o) {
     if constexpr (PREC == NR_PREC_BF16) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            o.s[0][j] = static_cast<__bf16>(a[j]);
-            o.s[1][j] = static_cast<__bf16>(a[8 + j]);
-        }
+        o.s[0] = pack8(a, 0);
+        o.s[1] = pack8(a, 1);
     } else {
         o.v = a;
     }
@@ -116,6 +130,156 @@ __device__ __forceinline__ void pe_feat_bwd(float x0, float x1, float x2, int f,
         g1 += d;
     else
         g2 += d;
+}
+
+// bf16 positional encoding.  sin/cos by the hardware v_sin_f32 (argument in
+// revolutions) after an exact two-term reduction: x/(2 pi) = hi + lo with
+// hi = x*C1 rounded and lo = fma(x, C1, -hi) + x*C2, so 2^k x/(2 pi) mod 1 =
+// fract(2^k hi) + 2^k lo (2^k hi exact).  Absolute error ~1e-6, far below the
+// bf16 rounding (2^-9 relative) the encoding goes through; the fp32 path keeps
+// sinf/cosf.  cos(v) = sin(v + 1/4 revolution).
+#ifndef NR_FASTPE
+#define NR_FASTPE 1
+#endif
+#ifndef NR_BIASMFMA
+#define NR_BIASMFMA 1
+#endif
+struct PeRev {
+    float x[3], hi[3], lo[3];
+};
+
+__device__ __forceinline__ PeRev pe_rev(float x0, float x1, float x2) {
+    constexpr float C1 = 0.15915494f, C2 = 6.4206382e-09f;  // fp32(1/2pi), 1/2pi - C1
+    PeRev p;
+    const float xs[3] = {x0, x1, x2};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        p.x[c] = xs[c];
+        p.hi[c] = xs[c] * C1;
+        p.lo[c] = fmaf(xs[c], C1, -p.hi[c]) + xs[c] * C2;
+    }
+    return p;
+}
+
+// feature f (compile-time after unrolling) for lane half 0 and f1 for half 1
+__device__ __forceinline__ float pe_fast(const PeRev& p, int f0, int f1, bool h1, int L) {
+    auto kind = [](int f) { return f < 3 ? 0 : 1; };
+    auto trig = [&](int f, float& hi, float& lo) {  // 2^k (hi, lo) + phase of feature f
+        const int fp = f - 3, k = fp / 6, rem = fp - 6 * k, c = rem % 3;
+        const float sc = static_cast<float>(1 << (k < 24 ? k : 0));
+        hi = p.hi[c] * sc;
+        lo = fmaf(p.lo[c], sc, rem < 3 ? 0.f : 0.25f);
+        return k < L;
+    };
+    if (kind(f0) == 1 && kind(f1) == 1) {
+        float h0, l0, hh, lh;
+        const bool v0 = trig(f0, h0, l0), v1 = trig(f1, hh, lh);
+        const float hi = h1 ? hh : h0, lo = h1 ? lh : l0;
+        const float v = __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(hi) + lo);
+        return (h1 ? v1 : v0) ? v : 0.f;
+    }
+    auto one = [&](int f) -> float {
+        if (f < 3) return p.x[f];
+        float hi, lo;
+        const bool ok = trig(f, hi, lo);
+        return ok ? __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(hi) + lo) : 0.f;
+    };
+    const float a0 = one(f0), a1 = one(f1);
+    return h1 ? a1 : a0;
+}
+
+// ---- bf16 epilogue: bias by MFMA, ReLU and mask bits on packed bf16 pairs ----
+// Bias of row block nb as an MFMA A fragment against an all-ones B operand:
+// lanes 0..31 hold bias[32 nb + lane] split exactly into bf16 hi + mid + lo,
+// lanes 32..63 zeros, so D += bias broadcast over the 32 samples of the tile.
+__device__ __forceinline__ bf16x8 bias_frag(float b) {
+    const unsigned w0 = cvt_pk_bf16(b, 0.f);               // hi
+    const float r1 = b - __uint_as_float(w0 << 16);
+    const unsigned w1 = cvt_pk_bf16(r1, 0.f);              // mid
+    const float r2 = r1 - __uint_as_float(w1 << 16);
+    const unsigned w2 = cvt_pk_bf16(r2, 0.f);              // lo
+    return __builtin_bit_cast(bf16x8, u32x4{w0 | (w1 << 16), w2, 0u, 0u});
+}
+
+__device__ __forceinline__ bf16x8 bf16_ones() {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = static_cast<__bf16>(1.0f);
+    return o;
+}
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// Word w (0..7) of a bf16 block holds accumulator registers 2w (low half) and
+// 2w+1 (high half).  bf16 ReLU = max as int16 against 0 (negative bf16 has the
+// sign bit set).  Mask bits of a layer, 4 words per lane: block nb, word w sets
+// bit j = 8 (nb & 1) + w (register 2w > 0) and bit 16 + j (register 2w+1 > 0)
+// of word nb >> 1.
+__device__ __forceinline__ unsigned relu_pk(unsigned w) {
+    return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(s16x2, w), s16x2{0, 0}));
+}
+// (asm: after the ReLU the compiler knows w >= 0 and rewrites the min into
+// per-half compares and selects, six instructions instead of one)
+__device__ __forceinline__ unsigned nz_pk(unsigned w) {
+    unsigned r;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(w), "s"(0x10001u));
+    return r;
+}
+
+// fp32 accumulators (bias included) -> bf16 B operands; ReLU in fp32 when a VALU
+// head reads the same activations, else on the packed pairs; optional mask bits.
+template <int NBO, bool RELU, bool RELU_F32, bool MASK>
+__device__ __forceinline__ void epi_bf16(f32x16 (&acc)[NBO], bf16x8 (&out)[NBO][2], unsigned (&mw)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) mw[q] = 0u;
+#pragma unroll
+    for (int nb = 0; nb < NBO; ++nb) {
+        if constexpr (RELU && RELU_F32)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[nb][r] = acc[nb][r] > 0.f ? acc[nb][r] : 0.f;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            u32x4 wd = __builtin_bit_cast(u32x4, pack8(acc[nb], hf));
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                if constexpr (RELU && !RELU_F32) wd[m] = relu_pk(wd[m]);
+                if constexpr (MASK) mw[nb >> 1] |= nz_pk(wd[m]) << (8 * (nb & 1) + 4 * hf + m);
+            }
+            out[nb][hf] = __builtin_bit_cast(bf16x8, wd);
+        }
+    }
+}
+
+// Backward: zero the packed dz pairs whose forward activation was not positive.
+__device__ __forceinline__ void mask_pk(bf16x8 (&v)[2], unsigned word, int nb) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+        u32x4 wd = __builtin_bit_cast(u32x4, v[hf]);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const unsigned t = (word >> (8 * (nb & 1) + 4 * hf + m)) & 0x10001u;
+            wd[m] &= t * 0xFFFFu;
+        }
+        v[hf] = __builtin_bit_cast(bf16x8, wd);
+    }
+}
+
+// dz block -> B operand with the ReLU mask of its forward activation applied
+// (bf16: packed-pair mask words of epi_bf16; fp32: bit (nb&1)*16 + r of word nb>>1).
+template <int PREC>
+__device__ __forceinline__ void to_in_masked(f32x16 a, const u32x4& mw, int nb, InBlk<PREC>& o) {
+    if constexpr (PREC == NR_PREC_BF16) {
+        to_in<PREC>(a, o);
+        mask_pk(o.s, mw[nb >> 1], nb);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const unsigned bit = (mw[nb >> 1] >> ((nb & 1) * 16 + r)) & 1u;
+            a[r] = bit ? a[r] : 0.f;
+        }
+        o.v = a;
+    }
 }
 
 // One 32-feature block of a tile as a B-operand image: FPB fragments of 1 KB.
@@ -442,6 +606,7 @@ struct FwdArgs {
     int slot_bytes;
     StreamDesc sd;  // W images: trunk 0..n-1, feat, dir
     int64_t vb[kMaxMfmaLayers];
+    int64_t bo[kMaxMfmaLayers];  // bias offsets in params (bf16: bias by MFMA)
     int64_t vsig, vrgb, sig_b, rgb_b;
     int64_t sv_off[kMaxTrunk + 4];
     int sv_feat, sv_denc, sv_hc;
@@ -492,6 +657,10 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
         for (int t = 0; t < TPW; ++t)
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
+        float bl[kHB];  // bf16: this layer's bias, lane < 32 holds rows 32 nb + lane
+        if constexpr (PREC == NR_PREC_BF16)
+#pragma unroll
+            for (int nb = 0; nb < kHB; ++nb) bl[nb] = lane < 32 ? a.params[a.bo[i] + 32 * nb + lane] : 0.f;
         const bool skip_in = i > 0 && ((a.skips >> (i - 1)) & 1u);
         if (i == 0 || skip_in) {
             // x_enc is not kept in registers: the skip layer reloads the saved
@@ -513,11 +682,15 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                 // layer loop (and spilled) as a loop invariant
                 float p0 = px[t][0], p1 = px[t][1], p2 = px[t][2];
                 asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2));
+                const PeRev pr = pe_rev(p0, p1, p2);
 #pragma unroll
                 for (int kb = 0; kb < XB; ++kb) {
                     f32x16 v;
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) v[r] = pe_feat(p0, p1, p2, 32 * kb + acc_row(r, h), a.L);
+                    for (int r = 0; r < 16; ++r)
+                        v[r] = (PREC == NR_PREC_BF16 && NR_FASTPE)
+                                   ? pe_fast(pr, 32 * kb + acc_row(r, 0), 32 * kb + acc_row(r, 1), h != 0, a.L)
+                                   : pe_feat(p0, p1, p2, 32 * kb + acc_row(r, h), a.L);
                     to_in<PREC>(v, xe.v[t][kb]);
                     if constexpr (TRAIN)
                         if (tok[t]) store_img<PREC>(a.saved + a.sv_off[SV_XENC], tile0 + t, XB, kb, xe.v[t][kb], lane);
@@ -530,12 +703,26 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                                                        sink_of(SV_H0 + i - 1, kHB));
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-            bias_act<kHB, true>(acc[t], vimg(a.packed, a.vb[i], lane), w);
+            if constexpr (PREC == NR_PREC_BF16) {
+                bf16x8 hv[kHB][2];
+                if (NR_BIASMFMA) {
 #pragma unroll
-            for (int nb = 0; nb < kHB; ++nb) {
-                InBlk<PREC> v;
-                to_in<PREC>(acc[t][nb], v);
-                hin.put(t, nb, v);
+                    for (int nb = 0; nb < kHB; ++nb) acc[t][nb] = mfma_bf16(bias_frag(bl[nb]), bf16_ones(), acc[t][nb]);
+                } else {
+                    unsigned wt[4];
+                    bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[i], lane), wt);
+                }
+                epi_bf16<kHB, true, false, TRAIN>(acc[t], hv, w);
+#pragma unroll
+                for (int nb = 0; nb < kHB; ++nb) hin.put(t, nb, InBlk<PREC>{{hv[nb][0], hv[nb][1]}});
+            } else {
+                bias_act<kHB, true>(acc[t], vimg(a.packed, a.vb[i], lane), w);
+#pragma unroll
+                for (int nb = 0; nb < kHB; ++nb) {
+                    InBlk<PREC> v;
+                    to_in<PREC>(acc[t][nb], v);
+                    hin.put(t, nb, v);
+                }
             }
             if constexpr (TRAIN)
                 if (tok[t]) masks[((tile0 + t) * a.n_mask + i) * 64 + lane] = u32x4{w[0], w[1], w[2], w[3]};
@@ -556,7 +743,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
 #pragma unroll
-                    for (int t = 0; t < TPW; ++t) sp[t] += wv[e] * acc[t][nb][4 * g + e];
+                    for (int t = 0; t < TPW; ++t) sp[t] += wv[e] * (acc[t][nb][4 * g + e] > 0.f ? acc[t][nb][4 * g + e] : 0.f);
             }
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
@@ -575,12 +762,28 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                                                sink_of(SV_H0 + n - 1, kHB));
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[n], lane), w);
+        if constexpr (PREC == NR_PREC_BF16) {
+            bf16x8 hv[kHB][2];
 #pragma unroll
-        for (int nb = 0; nb < kHB; ++nb) {
-            InBlk<PREC> v;
-            to_in<PREC>(acc[t][nb], v);
-            hin.put(t, nb, v);
+            for (int nb = 0; nb < kHB; ++nb) {
+                const float b = lane < 32 ? a.params[a.bo[n] + 32 * nb + lane] : 0.f;
+                if (NR_BIASMFMA) acc[t][nb] = mfma_bf16(bias_frag(b), bf16_ones(), acc[t][nb]);
+            }
+            if (!NR_BIASMFMA) {
+                unsigned wt[4];
+                bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[n], lane), wt);
+            }
+            epi_bf16<kHB, false, false, false>(acc[t], hv, w);
+#pragma unroll
+            for (int nb = 0; nb < kHB; ++nb) hin.put(t, nb, InBlk<PREC>{{hv[nb][0], hv[nb][1]}});
+        } else {
+            bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[n], lane), w);
+#pragma unroll
+            for (int nb = 0; nb < kHB; ++nb) {
+                InBlk<PREC> v;
+                to_in<PREC>(acc[t][nb], v);
+                hin.put(t, nb, v);
+            }
         }
     }
 
@@ -601,11 +804,15 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
             const bool valid = m < a.M;
             const float d0 = valid ? a.d[3 * m] : 0.f, d1 = valid ? a.d[3 * m + 1] : 0.f,
                         d2 = valid ? a.d[3 * m + 2] : 0.f;
+            const PeRev pr = pe_rev(d0, d1, d2);
 #pragma unroll
             for (int kb = 0; kb < DB; ++kb) {
                 f32x16 v;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = pe_feat(d0, d1, d2, 32 * kb + acc_row(r, h), a.Ld);
+                for (int r = 0; r < 16; ++r)
+                    v[r] = (PREC == NR_PREC_BF16 && NR_FASTPE)
+                               ? pe_fast(pr, 32 * kb + acc_row(r, 0), 32 * kb + acc_row(r, 1), h != 0, a.Ld)
+                               : pe_feat(d0, d1, d2, 32 * kb + acc_row(r, h), a.Ld);
                 to_in<PREC>(v, de.v[t][kb]);
                 if constexpr (TRAIN)
                     if (tok[t]) store_img<PREC>(a.saved + a.sv_off[a.sv_denc], tile0 + t, DB, kb, de.v[t][kb], lane);
@@ -615,13 +822,30 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        bias_act<NC, true>(ac[t], vimg(a.packed, a.vb[n + 1], lane), w);
+        bf16x8 hcv[NC][2];
+        if constexpr (PREC == NR_PREC_BF16) {
+#pragma unroll
+            for (int nb = 0; nb < NC; ++nb) {
+                const float b = lane < 32 ? a.params[a.bo[n + 1] + 32 * nb + lane] : 0.f;
+                if (NR_BIASMFMA) ac[t][nb] = mfma_bf16(bias_frag(b), bf16_ones(), ac[t][nb]);
+            }
+            if (!NR_BIASMFMA) {
+                unsigned wt[4];
+                bias_act<NC, false>(ac[t], vimg(a.packed, a.vb[n + 1], lane), wt);
+            }
+            epi_bf16<NC, true, true, TRAIN>(ac[t], hcv, w);
+        } else {
+            bias_act<NC, true>(ac[t], vimg(a.packed, a.vb[n + 1], lane), w);
+        }
         if constexpr (TRAIN) {
             if (tok[t]) {
 #pragma unroll
                 for (int nb = 0; nb < NC; ++nb) {
                     InBlk<PREC> v;
-                    to_in<PREC>(ac[t][nb], v);
+                    if constexpr (PREC == NR_PREC_BF16)
+                        v = InBlk<PREC>{{hcv[nb][0], hcv[nb][1]}};
+                    else
+                        to_in<PREC>(ac[t][nb], v);
                     store_img<PREC>(a.saved + a.sv_off[a.sv_hc], tile0 + t, NC, nb, v, lane);
                 }
                 masks[((tile0 + t) * a.n_mask + n) * 64 + lane] = u32x4{w[0], w[1], w[2], w[3]};
@@ -757,10 +981,10 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) dc[nb][4 * g + e] = (w0[e] * dr[0] + w1[e] * dr[1]) + w2[e] * dr[2];
             }
-        apply_mask<NC>(dc, mask_of(t, n));
+        const u32x4 mwc = mask_of(t, n);
 #pragma unroll
         for (int nb = 0; nb < NC; ++nb) {
-            to_in<PREC>(dc[nb], cin.v[t][nb]);
+            to_in_masked<PREC>(dc[nb], mwc, nb, cin.v[t][nb]);
             put_dz(a.ws_dir, NC, t, nb, cin.v[t][nb]);
         }
     }
@@ -841,11 +1065,11 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        apply_mask<kHB>(acc[t], mask_of(t, n - 1));
+        const u32x4 mwf = mask_of(t, n - 1);
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb) {
             InBlk<PREC> v;
-            to_in<PREC>(acc[t][nb], v);
+            to_in_masked<PREC>(acc[t][nb], mwf, nb, v);
             hin.put(t, nb, v);
             if ((n == 1 && !WANT_X) || !NR_SINK_BWD)  // (dz_0 without g_x has no consumer stream)
                 store_dz(WS_DZ0 + n - 1, kHB, t, nb, v);
@@ -879,11 +1103,11 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
         }
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-            apply_mask<kHB>(acc[t], mask_of(t, i - 1));
+            const u32x4 mwt = mask_of(t, i - 1);
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) {
                 InBlk<PREC> v;
-                to_in<PREC>(acc[t][nb], v);
+                to_in_masked<PREC>(acc[t][nb], mwt, nb, v);
                 hin.put(t, nb, v);
                 if ((i == 1 && !WANT_X) || !NR_SINK_BWD)  // (dz_0 without g_x has no consumer stream)
                     store_dz(WS_DZ0 + i - 1, kHB, t, nb, v);
@@ -1664,6 +1888,7 @@ int nr_mlp_forward(const NrMlpConfig* cfg, const void* packed, const float* para
         const LinearDesc& dl = p.lin[l];
         add_stream_layer(a.sd, dl.KB, dl.NB * p.fpb);
         a.vb[l] = dl.vb;
+        a.bo[l] = dl.b_off;
     }
     a.vsig = p.vsig;
     a.vrgb = p.vrgb;
