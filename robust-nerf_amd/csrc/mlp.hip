@@ -237,7 +237,7 @@ __device__ __forceinline__ void epi_bf16(f32x16 (&acc)[NBO], bf16x8 (&out)[NBO][
     for (int nb = 0; nb < NBO; ++nb) {
         if constexpr (RELU && RELU_F32)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[nb][r] = acc[nb][r] > 0.f ? acc[nb][r] : 0.f;
+            for (int r = 0; r < 16; ++r) acc[nb][r] = __int_as_float(max(__float_as_int(acc[nb][r]), 0));
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             u32x4 wd = __builtin_bit_cast(u32x4, pack8(acc[nb], hf));
@@ -345,6 +345,25 @@ __device__ __forceinline__ VImg vimg(const char* packed, int64_t off, int lane) 
     return VImg{(cfloat*)(q), (lane >> 5) != 0};
 }
 #define NR_VEC(img, nb, g) ((img).g4((nb), (g)))
+
+// Pair images (w_sigma, the rows of W_rgb): element nb*16 + r holds the weights of
+// accumulator register r of block nb for lane half 0 and for lane half 1, read with
+// one 64-bit scalar load; a packed FMA evaluates both halves and each lane keeps
+// its own (no per-lane selects of scalar weights: VOP3 reads one SGPR at most).
+typedef const __attribute__((address_space(4))) f32x2 cf32x2;
+struct PImg {
+    cf32x2* p;
+    __device__ __forceinline__ f32x2 at(int nb, int r) const { return p[nb * 16 + r]; }
+};
+__device__ __forceinline__ PImg pimg(const char* packed, int64_t off) {
+    const char* q = packed + off;
+    asm volatile("" : "+s"(q));
+    return PImg{(cf32x2*)(q)};
+}
+__device__ __forceinline__ f32x2 bcast2(float x) { return f32x2{x, x}; }
+// ReLU as an integer max (negative floats, -0 included, are negative as int32):
+// one v_max_i32, where the float compare-select also canonicalises its input
+__device__ __forceinline__ float relu_f(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
 
 template <int NBO, bool RELU>
 __device__ __forceinline__ void bias_act(f32x16 (&acc)[NBO], const VImg& bias, unsigned (&w)[4]) {
@@ -732,19 +751,17 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     // sigma head (VALU): relu(w_sigma . h + b), from the fp32 activations
     float sp[TPW];
     {
-        const VImg ws = vimg(a.packed, a.vsig, lane);
+        const PImg ws = pimg(a.packed, a.vsig);
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) sp[t] = 0.f;
+        for (int t = 0; t < TPW; ++t) {
+            f32x2 s2 = {0.f, 0.f};
 #pragma unroll
-        for (int nb = 0; nb < kHB; ++nb)
+            for (int nb = 0; nb < kHB; ++nb)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 wv = NR_VEC(ws, nb, g);
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int t = 0; t < TPW; ++t) sp[t] += wv[e] * (acc[t][nb][4 * g + e] > 0.f ? acc[t][nb][4 * g + e] : 0.f);
-            }
+                for (int r = 0; r < 16; ++r)
+                    s2 = __builtin_elementwise_fma(bcast2(relu_f(acc[t][nb][r])), ws.at(nb, r), s2);
+            sp[t] = h ? s2[1] : s2[0];
+        }
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
             sp[t] += __shfl_xor(sp[t], 32);
@@ -855,16 +872,13 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
         float pr[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const VImg wr = vimg(a.packed, a.vrgb + c * NC * 128, lane);
-            float s = 0.f;
+            const PImg wr = pimg(a.packed, a.vrgb + c * NC * 128);
+            f32x2 s2 = {0.f, 0.f};
 #pragma unroll
             for (int nb = 0; nb < NC; ++nb)
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const f32x4 wv = NR_VEC(wr, nb, g);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) s += wv[e] * ac[t][nb][4 * g + e];
-                }
+                for (int r = 0; r < 16; ++r) s2 = __builtin_elementwise_fma(bcast2(ac[t][nb][r]), wr.at(nb, r), s2);
+            float s = h ? s2[1] : s2[0];
             s += __shfl_xor(s, 32);
             s = s + a.params[a.rgb_b + c];
             pr[c] = 1.0f / (1.0f + expf(-s));
@@ -972,14 +986,16 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
         }
         // dz_c = (W_rgb^T dz_rgb) * [h_c > 0]
         f32x16 dc[NC];
-        const VImg wr = vimg(a.packed, a.vrgb, lane);
+        const PImg wr0 = pimg(a.packed, a.vrgb), wr1 = pimg(a.packed, a.vrgb + NC * 128),
+                   wr2 = pimg(a.packed, a.vrgb + 2 * NC * 128);
 #pragma unroll
         for (int nb = 0; nb < NC; ++nb)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 w0 = NR_VEC(wr, nb, g), w1 = NR_VEC(wr, NC + nb, g), w2 = NR_VEC(wr, 2 * NC + nb, g);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) dc[nb][4 * g + e] = (w0[e] * dr[0] + w1[e] * dr[1]) + w2[e] * dr[2];
+            for (int r = 0; r < 16; ++r) {
+                f32x2 v = wr0.at(nb, r) * bcast2(dr[0]);
+                v = __builtin_elementwise_fma(wr1.at(nb, r), bcast2(dr[1]), v);
+                v = __builtin_elementwise_fma(wr2.at(nb, r), bcast2(dr[2]), v);
+                dc[nb][r] = h ? v[1] : v[0];
             }
         const u32x4 mwc = mask_of(t, n);
 #pragma unroll
@@ -1051,17 +1067,16 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane,
                                                sink_of(a.ws_feat, kHB));
     {
-        const VImg ws = vimg(a.packed, a.vsig, lane);
+        const PImg ws = pimg(a.packed, a.vsig);
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 wv = NR_VEC(ws, nb, g);
+            for (int r = 0; r < 16; ++r)
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int t = 0; t < TPW; ++t) acc[t][nb][4 * g + e] = acc[t][nb][4 * g + e] + wv[e] * dzs[t];
-            }
+                for (int t = 0; t < TPW; ++t) {
+                    const f32x2 v = __builtin_elementwise_fma(ws.at(nb, r), bcast2(dzs[t]), bcast2(acc[t][nb][r]));
+                    acc[t][nb][r] = h ? v[1] : v[0];
+                }
     }
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
@@ -1623,6 +1638,7 @@ struct PackVecArgs {
     int len[kMaxMfmaLayers + 4];              // valid features
     int64_t dst[kMaxMfmaLayers + 4];          // byte offset in packed
     int cum[kMaxMfmaLayers + 5];              // image elements (NB*32) prefix
+    int pair[kMaxMfmaLayers + 4];             // 1: pair image (PImg), 0: vector image (VImg)
 };
 
 __global__ void mlp_pack_vec_kernel(PackVecArgs a) {
@@ -1631,7 +1647,8 @@ __global__ void mlp_pack_vec_kernel(PackVecArgs a) {
     int v = 0;
     while (g >= a.cum[v + 1]) ++v;
     const int idx = g - a.cum[v];
-    const int f = 32 * (idx >> 5) + acc_row(idx & 15, (idx >> 4) & 1);
+    const int f = a.pair[v] ? 32 * (idx >> 5) + acc_row((idx >> 1) & 15, idx & 1)
+                            : 32 * (idx >> 5) + acc_row(idx & 15, (idx >> 4) & 1);
     reinterpret_cast<float*>(a.packed + a.dst[v])[idx] = f < a.len[v] ? a.params[a.src[v] + f] : 0.f;
 }
 
@@ -1809,7 +1826,8 @@ int nr_mlp_pack(const NrMlpConfig* cfg, const float* params, void* packed, nr_st
     std::memset(&v, 0, sizeof(v));
     v.params = params;
     v.packed = static_cast<char*>(packed);
-    auto add_vec = [&](int64_t src, int len, int64_t dst, int nblk) {
+    auto add_vec = [&](int64_t src, int len, int64_t dst, int nblk, int pair = 0) {
+        v.pair[v.nv] = pair;
         v.src[v.nv] = src;
         v.len[v.nv] = len;
         v.dst[v.nv] = dst;
@@ -1817,8 +1835,9 @@ int nr_mlp_pack(const NrMlpConfig* cfg, const float* params, void* packed, nr_st
         v.nv++;
     };
     for (int l = 0; l < p.n_lin; ++l) add_vec(p.lin[l].b_off, p.lin[l].out, p.lin[l].vb, p.lin[l].NB);
-    add_vec(p.sig_w, kHidden, p.vsig, kHB);
-    for (int c = 0; c < 3; ++c) add_vec(p.rgb_w + c * (kHidden / 2), kHidden / 2, p.vrgb + c * (kHidden / 2) * 4, kHB / 2);
+    add_vec(p.sig_w, kHidden, p.vsig, kHB, 1);
+    for (int c = 0; c < 3; ++c)
+        add_vec(p.rgb_w + c * (kHidden / 2), kHidden / 2, p.vrgb + c * (kHidden / 2) * 4, kHB / 2, 1);
     hipLaunchKernelGGL(mlp_pack_vec_kernel, dim3(ceil_div(v.cum[v.nv], 256)), dim3(256), 0, s, v);
     NR_LAUNCH_CHECK("nr_mlp_pack");
     if (p.fast_ok) {
