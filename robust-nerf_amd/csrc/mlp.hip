@@ -138,6 +138,12 @@ __device__ __forceinline__ void pe_feat_bwd(float x0, float x1, float x2, int f,
 // fract(2^k hi) + 2^k lo (2^k hi exact).  Absolute error ~1e-6, far below the
 // bf16 rounding (2^-9 relative) the encoding goes through; the fp32 path keeps
 // sinf/cosf.  cos(v) = sin(v + 1/4 revolution).
+#ifndef NR_NT_STORE
+#define NR_NT_STORE 1
+#endif
+#ifndef NR_FWD_NOSINK
+#define NR_FWD_NOSINK 0  // A/B only: skip the saved-activation stores of the training forward
+#endif
 #ifndef NR_FASTPE
 #define NR_FASTPE 1
 #endif
@@ -289,8 +295,15 @@ __device__ __forceinline__ void store_img(char* __restrict__ region, int64_t til
     // wave-uniform base (tile is per wave) + the lane's 16 B: saddr + voffset stores
     char* base = region + ((tile * nblk + blk) * kFPB<PREC>) * static_cast<int64_t>(kFragBytes) + lane16();
     if constexpr (PREC == NR_PREC_BF16) {
+#if NR_NT_STORE
+        // streaming (non-temporal) stores: the 4 GB of images must not evict the
+        // L2-resident weight stream every workgroup re-reads
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v.s[0]), reinterpret_cast<u32x4*>(base));
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v.s[1]), reinterpret_cast<u32x4*>(base + kFragBytes));
+#else
         *reinterpret_cast<bf16x8*>(base) = v.s[0];
         *reinterpret_cast<bf16x8*>(base + kFragBytes) = v.s[1];
+#endif
     } else {
 #pragma unroll
         for (int tq = 0; tq < 4; ++tq)
@@ -657,7 +670,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     for (int t = 0; t < TPW; ++t) tokm |= (tok[t] ? 1u : 0u) << t;
     // training saves each layer input as the next stream consumes it
     auto sink_of = [&](int sv, int nblk) {
-        return Sink<PREC, TPW>{TRAIN ? a.saved + a.sv_off[sv] : nullptr, nblk, tile0, tokm};
+        return Sink<PREC, TPW>{(TRAIN && !NR_FWD_NOSINK) ? a.saved + a.sv_off[sv] : nullptr, nblk, tile0, tokm};
     };
 
     Ring ring{lds, a.slot_bytes, 0, nullptr, wv};
