@@ -114,6 +114,196 @@ __global__ void composite_bwd_kernel(const float* rgb, const float* sigma, const
     }
 }
 
+// ---- wave-per-ray forms (S <= 64 * kCompK): one 64-lane wave per ray, lane j
+// owns samples [jK, jK + K) (K = ceil(S / 64)), all loads contiguous per lane.
+// Transmittance: lane-local running product times the wave's exclusive product
+// scan of the per-lane products (the thread-per-ray kernels above walk the ray
+// serially through strided loads: 64 rays per launch-wide wave set, latency-bound).
+// The backward's reverse recurrence R_i = u_{i+1} + t_{i+1} R_{i+1} (u = G a)
+// becomes a lane-local affine map R_i = A_i + B_i X_j of the lane's boundary value
+// X_j, and X_j = alpha_{j+1} + beta_{j+1} X_{j+1} is a suffix scan of affine maps
+// across lanes.  Samples past S are padded with a = 0, t = 1, G = 0.  Only the
+// association of the products and sums differs from the serial walk.
+constexpr int kCompK = 8;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void composite_fwd_wave_kernel(const float* rgb, const float* sigma,
+                                                                 const float* z, const float* rd,
+                                                                 const float* noise, int B, int S, int K,
+                                                                 int white, float* rgb_map, float* depth,
+                                                                 float* acc, float* weights) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (b >= B) return;  // wave-uniform
+    const float dnorm = sqrtf(rd[3 * b] * rd[3 * b] + rd[3 * b + 1] * rd[3 * b + 1] + rd[3 * b + 2] * rd[3 * b + 2]);
+    const int64_t base = static_cast<int64_t>(b) * S;
+    const int i0 = lane * K;
+    float al[kCompK], L[kCompK];
+    float P = 1.0f;
+#pragma unroll
+    for (int k = 0; k < kCompK; ++k) {
+        al[k] = 0.f;
+        L[k] = P;
+        const int i = i0 + k;
+        if (k < K && i < S) {
+            const SampleTerms st = sample_terms(sigma, z, noise, base, i, S, dnorm);
+            al[k] = st.alpha;
+            P = P * (1.0f - st.alpha + 1e-10f);
+        }
+    }
+    // exclusive product scan of P over lanes
+    float incl = P;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const float o = __shfl_up(incl, d);
+        if (lane >= d) incl *= o;
+    }
+    float E = __shfl_up(incl, 1);
+    if (lane == 0) E = 1.0f;
+    float r = 0.f, g = 0.f, bl = 0.f, dd = 0.f, a = 0.f;
+#pragma unroll
+    for (int k = 0; k < kCompK; ++k) {
+        const int i = i0 + k;
+        if (k < K && i < S) {
+            const float w = al[k] * (E * L[k]);
+            if (weights) weights[base + i] = w;
+            const int64_t q = 3 * (base + i);
+            r += w * rgb[q];
+            g += w * rgb[q + 1];
+            bl += w * rgb[q + 2];
+            dd += w * z[base + i];
+            a += w;
+        }
+    }
+    r = wave_sum(r);
+    g = wave_sum(g);
+    bl = wave_sum(bl);
+    dd = wave_sum(dd);
+    a = wave_sum(a);
+    if (lane == 0) {
+        if (white) {
+            r = r + (1.0f - a);
+            g = g + (1.0f - a);
+            bl = bl + (1.0f - a);
+        }
+        rgb_map[3 * b] = r;
+        rgb_map[3 * b + 1] = g;
+        rgb_map[3 * b + 2] = bl;
+        if (depth) depth[b] = dd;
+        if (acc) acc[b] = a;
+    }
+}
+
+__global__ __launch_bounds__(256) void composite_bwd_wave_kernel(
+    const float* rgb, const float* sigma, const float* z, const float* rd, const float* noise, int B, int S, int K,
+    int white, const float* g_map, const float* g_depth, const float* g_acc, const float* g_w, float* g_rgb,
+    float* g_sigma, float* g_rd) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (b >= B) return;
+    const float dx = rd[3 * b], dy = rd[3 * b + 1], dz = rd[3 * b + 2];
+    const float dnorm = sqrtf(dx * dx + dy * dy + dz * dz);
+    const int64_t base = static_cast<int64_t>(b) * S;
+    const float gr = g_map[3 * b], gg = g_map[3 * b + 1], gb = g_map[3 * b + 2];
+    const float gd = g_depth ? g_depth[b] : 0.f;
+    const float ga = (g_acc ? g_acc[b] : 0.f) - (white ? (gr + gg) + gb : 0.f);
+    const int i0 = lane * K;
+    float al[kCompK], tt[kCompK], ee[kCompK], sg[kCompK], dr[kCompK], GG[kCompK], L[kCompK];
+    float P = 1.0f;
+#pragma unroll
+    for (int k = 0; k < kCompK; ++k) {
+        al[k] = 0.f;
+        tt[k] = 1.0f;
+        ee[k] = 1.0f;
+        sg[k] = 0.f;
+        dr[k] = 0.f;
+        GG[k] = 0.f;
+        L[k] = P;
+        const int i = i0 + k;
+        if (k < K && i < S) {
+            const SampleTerms st = sample_terms(sigma, z, noise, base, i, S, dnorm);
+            al[k] = st.alpha;
+            tt[k] = 1.0f - st.alpha + 1e-10f;
+            ee[k] = st.e;
+            sg[k] = st.sig;
+            dr[k] = st.delta_raw;
+            const int64_t q = 3 * (base + i);
+            float G = ((gr * rgb[q] + gg * rgb[q + 1]) + gb * rgb[q + 2]) + gd * z[base + i] + ga;
+            if (g_w) G += g_w[base + i];
+            GG[k] = G;
+            P = P * tt[k];
+        }
+    }
+    float incl = P;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const float o = __shfl_up(incl, d);
+        if (lane >= d) incl *= o;
+    }
+    float E = __shfl_up(incl, 1);
+    if (lane == 0) E = 1.0f;
+    // lane-local affine maps R_i = A_i + B_i X (X = R at the lane's last sample)
+    float A[kCompK], Bc[kCompK];
+    float an = 0.f, bn = 1.0f;
+#pragma unroll
+    for (int k = kCompK - 1; k >= 0; --k) {
+        if (k < K) {
+            if (k == K - 1) {
+                an = 0.f;
+                bn = 1.0f;
+            } else {
+                an = GG[k + 1] * al[k + 1] + tt[k + 1] * an;
+                bn = tt[k + 1] * bn;
+            }
+        }
+        A[k] = an;
+        Bc[k] = bn;
+    }
+    // this lane's map for its predecessor: X_{j-1} = alpha + beta X_j
+    float qa = GG[0] * al[0] + tt[0] * A[0];
+    float qb = tt[0] * Bc[0];
+    // suffix composition Q_j = N_j o N_{j+1} o ... o N_63
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const float oa = __shfl_down(qa, d), ob = __shfl_down(qb, d);
+        if (lane + d < 64) {
+            qa = qa + qb * oa;
+            qb = qb * ob;
+        }
+    }
+    float X = __shfl_down(qa, 1);
+    if (lane == 63) X = 0.f;
+    float g_norm = 0.f;
+#pragma unroll
+    for (int k = 0; k < kCompK; ++k) {
+        const int i = i0 + k;
+        if (k < K && i < S) {
+            const float Ti = E * L[k];
+            const float w = al[k] * Ti;
+            const int64_t q = 3 * (base + i);
+            g_rgb[q] = gr * w;
+            g_rgb[q + 1] = gg * w;
+            g_rgb[q + 2] = gb * w;
+            const float R = A[k] + Bc[k] * X;
+            const float g_alpha = Ti * (GG[k] - R);
+            const float g_x = -g_alpha * ee[k];
+            g_sigma[base + i] = (sg[k] > 0.f) ? -g_x * (dr[k] * dnorm) : 0.f;
+            g_norm += g_x * (-sg[k] * dr[k]);
+        }
+    }
+    g_norm = wave_sum(g_norm);
+    if (g_rd && lane == 0) {
+        g_rd[3 * b] += g_norm * dx / dnorm;
+        g_rd[3 * b + 1] += g_norm * dy / dnorm;
+        g_rd[3 * b + 2] += g_norm * dz / dnorm;
+    }
+}
+
 // loss = mean((p - t)^2) over n = 3B; g = 2 (p - t) / n * scale.  One block.
 __global__ void mse_kernel(const float* p, const float* t, int n, float scale, float* loss, float* g) {
     __shared__ float part[16];
@@ -146,8 +336,13 @@ int nr_composite_fwd(const float* rgb, const float* sigma, const float* z, const
                      nr_stream_t stream) {
     NR_REQUIRE(rgb && sigma && z && rd && rgb_map && B >= 0 && S > 0, "nr_composite_fwd: bad arguments");
     if (B == 0) return NR_OK;
-    hipLaunchKernelGGL(composite_fwd_kernel, dim3(ceil_div(B, 64)), dim3(64), 0, static_cast<hipStream_t>(stream),
-                       rgb, sigma, z, rd, noise, B, S, white, rgb_map, depth, acc, weights);
+    if (S <= 64 * kCompK)
+        hipLaunchKernelGGL(composite_fwd_wave_kernel, dim3(ceil_div(B, 4)), dim3(256), 0,
+                           static_cast<hipStream_t>(stream), rgb, sigma, z, rd, noise, B, S, (S + 63) / 64, white,
+                           rgb_map, depth, acc, weights);
+    else
+        hipLaunchKernelGGL(composite_fwd_kernel, dim3(ceil_div(B, 64)), dim3(64), 0, static_cast<hipStream_t>(stream),
+                           rgb, sigma, z, rd, noise, B, S, white, rgb_map, depth, acc, weights);
     NR_LAUNCH_CHECK("nr_composite_fwd");
     return NR_OK;
 }
@@ -158,8 +353,13 @@ int nr_composite_bwd(const float* rgb, const float* sigma, const float* z, const
     NR_REQUIRE(rgb && sigma && z && rd && g_map && g_rgb && g_sigma && B >= 0 && S > 0,
                "nr_composite_bwd: bad arguments");
     if (B == 0) return NR_OK;
-    hipLaunchKernelGGL(composite_bwd_kernel, dim3(ceil_div(B, 64)), dim3(64), 0, static_cast<hipStream_t>(stream),
-                       rgb, sigma, z, rd, noise, B, S, white, g_map, g_depth, g_acc, g_w, g_rgb, g_sigma, g_rd);
+    if (S <= 64 * kCompK)
+        hipLaunchKernelGGL(composite_bwd_wave_kernel, dim3(ceil_div(B, 4)), dim3(256), 0,
+                           static_cast<hipStream_t>(stream), rgb, sigma, z, rd, noise, B, S, (S + 63) / 64, white,
+                           g_map, g_depth, g_acc, g_w, g_rgb, g_sigma, g_rd);
+    else
+        hipLaunchKernelGGL(composite_bwd_kernel, dim3(ceil_div(B, 64)), dim3(64), 0, static_cast<hipStream_t>(stream),
+                           rgb, sigma, z, rd, noise, B, S, white, g_map, g_depth, g_acc, g_w, g_rgb, g_sigma, g_rd);
     NR_LAUNCH_CHECK("nr_composite_bwd");
     return NR_OK;
 }

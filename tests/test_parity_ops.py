@@ -138,11 +138,15 @@ def test_positional_encoding_fwd_bwd():
     assert torch.allclose(xg.grad.cpu(), xr.grad, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("white,noise", [(True, False), (False, False), (True, True)])
-def test_composite_fwd_bwd(white, noise):
+@pytest.mark.parametrize("white,noise,S", [(True, False, 192), (False, False, 192), (True, True, 192),
+                                           (True, False, 64), (True, False, 384), (False, True, 130),
+                                           (True, False, 600)])
+def test_composite_fwd_bwd(white, noise, S):
+    """raw2outputs fwd/bwd (rendering.py:20-116): wave-per-ray scan kernels for
+    S <= 512 (incl. ragged S), the serial kernel above."""
     from noisy_src.rendering import raw2outputs
     g = torch.Generator().manual_seed(9)
-    B, S = 300, 192
+    B = 300
     o, d = _rays(B, seed=10)
     d = d * (1 + 0.1 * torch.rand(B, 1, generator=g))  # non-unit |d| exercises dists*|d|
     z = torch.sort(torch.rand(B, S, generator=g) * 4 + 2, dim=-1).values
