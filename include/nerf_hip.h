@@ -151,6 +151,7 @@ typedef struct NrMlpConfig {
 
 #define NR_PREC_FP32 0
 #define NR_PREC_BF16 1
+#define NR_PREC_FP16 2  /* cfg #5: fp16 MFMA operands, fp32 accumulate, 2^14 backward loss scale */
 
 /* Sizes (bytes unless stated).  M = number of samples. */
 int64_t nr_mlp_param_count(const NrMlpConfig* cfg);

@@ -435,23 +435,29 @@ def compute_pose_error(pose_gt, pose_noisy):
 
 
 class _Bf16OperandLinear(nn.Module):
-    """nn.Linear whose input and weight are rounded to bf16 (fp32 accumulate, fp32 bias):
-    the operand precision of the MI355X bf16 MFMA path, used as its parity reference."""
+    """nn.Linear whose input and weight are rounded to bf16 (or fp16) (fp32 accumulate,
+    fp32 bias): the operand precision of the MI355X 16-bit MFMA paths, used as their
+    parity reference."""
 
-    def __init__(self, lin: nn.Linear):
+    def __init__(self, lin: nn.Linear, dtype=torch.bfloat16):
         super().__init__()
         self.lin = lin
+        self.dtype = dtype
 
     def forward(self, x):
-        return F.linear(x.bfloat16().float(), self.lin.weight.bfloat16().float(), self.lin.bias)
+        return F.linear(x.to(self.dtype).float(), self.lin.weight.to(self.dtype).float(), self.lin.bias)
 
 
-def bf16_operand_nerf(model: "NeRF") -> "NeRF":
-    """Copy of an oracle NeRF whose MFMA layers (trunk, feature, dir) use bf16 operands."""
+def bf16_operand_nerf(model: "NeRF", dtype=torch.bfloat16) -> "NeRF":
+    """Copy of an oracle NeRF whose MFMA layers (trunk, feature, dir) use bf16 (or fp16) operands."""
     import copy
     emu = copy.deepcopy(model)
     for i in range(len(emu.pts_linears)):
-        emu.pts_linears[i] = _Bf16OperandLinear(emu.pts_linears[i])
-    emu.feature_linear = _Bf16OperandLinear(emu.feature_linear)
-    emu.dir_linear = _Bf16OperandLinear(emu.dir_linear)
+        emu.pts_linears[i] = _Bf16OperandLinear(emu.pts_linears[i], dtype)
+    emu.feature_linear = _Bf16OperandLinear(emu.feature_linear, dtype)
+    emu.dir_linear = _Bf16OperandLinear(emu.dir_linear, dtype)
     return emu
+
+
+def fp16_operand_nerf(model: "NeRF") -> "NeRF":
+    return bf16_operand_nerf(model, torch.float16)

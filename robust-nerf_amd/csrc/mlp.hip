@@ -33,10 +33,13 @@
 
 namespace nr {
 
+// 16-bit MFMA operands (bf16 or fp16; both stored as 16-bit patterns in bf16x8
+// registers, the MFMA and the conversions pick the format) or fp32.
 template <int PREC>
-struct InBlk;
-template <>
-struct InBlk<NR_PREC_BF16> {
+constexpr bool k16 = PREC != NR_PREC_FP32;
+
+template <int PREC>
+struct InBlk {
     bf16x8 s[2];
 };
 template <>
@@ -45,7 +48,25 @@ struct InBlk<NR_PREC_FP32> {
 };
 
 template <int PREC>
-constexpr int kFPB = PREC == NR_PREC_BF16 ? 2 : 4;  // 1-KB fragments per 32x32 block
+constexpr int kFPB = k16<PREC> ? 2 : 4;  // 1-KB fragments per 32x32 block
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// fp16 backward runs on dz scaled by 2^14 (the per-sample gradients of a mean
+// loss over 4096 rays sit near 1e-6, in fp16's subnormal range); the dW reduce and
+// the input gradients divide it out exactly.
+inline float grad_scale(int prec) { return prec == NR_PREC_FP16 ? 16384.0f : 1.0f; }
+
+// D += A.B on 16-bit operand images of either format
+template <int PREC>
+__device__ __forceinline__ f32x16 mfma16(bf16x8 a, bf16x8 b, f32x16 c) {
+    if constexpr (PREC == NR_PREC_FP16)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                      0, 0, 0);
+    else
+        return mfma_bf16(a, b, c);
+}
 
 // Two fp32 -> one word of two bf16 (RNE), low half = lo: one v_cvt_pk_bf16_f32
 // (element-wise casts compile to one convert per element plus a v_perm per pair;
@@ -55,20 +76,36 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned cvt_pk_bf16(float lo, float hi) {
     return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
 }
+template <int PREC>
+__device__ __forceinline__ unsigned cvt_pk16(float lo, float hi) {
+    if constexpr (PREC == NR_PREC_FP16)
+        return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{lo, hi}, f16x2));
+    else
+        return cvt_pk_bf16(lo, hi);
+}
+// 16-bit pattern of x (round to nearest even)
+template <int PREC>
+__device__ __forceinline__ float from16_lo(unsigned w) {
+    if constexpr (PREC == NR_PREC_FP16)
+        return static_cast<float>(__builtin_bit_cast(f16x2, w)[0]);
+    else
+        return __uint_as_float(w << 16);
+}
 
-// registers 8 hf .. 8 hf + 7 of an accumulator as a bf16x8 operand
+// registers 8 hf .. 8 hf + 7 of an accumulator as a 16-bit operand
+template <int PREC = NR_PREC_BF16>
 __device__ __forceinline__ bf16x8 pack8(const f32x16& a, int hf) {
     u32x4 w;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) w[m] = cvt_pk_bf16(a[8 * hf + 2 * m], a[8 * hf + 2 * m + 1]);
+    for (int m = 0; m < 4; ++m) w[m] = cvt_pk16<PREC>(a[8 * hf + 2 * m], a[8 * hf + 2 * m + 1]);
     return __builtin_bit_cast(bf16x8, w);
 }
 
 template <int PREC>
 __device__ __forceinline__ void to_in(const f32x16& a, InBlk<PREC>& o) {
-    if constexpr (PREC == NR_PREC_BF16) {
-        o.s[0] = pack8(a, 0);
-        o.s[1] = pack8(a, 1);
+    if constexpr (k16<PREC>) {
+        o.s[0] = pack8<PREC>(a, 0);
+        o.s[1] = pack8<PREC>(a, 1);
     } else {
         o.v = a;
     }
@@ -198,20 +235,20 @@ __device__ __forceinline__ float pe_fast(const PeRev& p, int f0, int f1, bool h1
 // Bias of row block nb as an MFMA A fragment against an all-ones B operand:
 // lanes 0..31 hold bias[32 nb + lane] split exactly into bf16 hi + mid + lo,
 // lanes 32..63 zeros, so D += bias broadcast over the 32 samples of the tile.
+template <int PREC>
 __device__ __forceinline__ bf16x8 bias_frag(float b) {
-    const unsigned w0 = cvt_pk_bf16(b, 0.f);               // hi
-    const float r1 = b - __uint_as_float(w0 << 16);
-    const unsigned w1 = cvt_pk_bf16(r1, 0.f);              // mid
-    const float r2 = r1 - __uint_as_float(w1 << 16);
-    const unsigned w2 = cvt_pk_bf16(r2, 0.f);              // lo
+    const unsigned w0 = cvt_pk16<PREC>(b, 0.f);            // hi
+    const float r1 = b - from16_lo<PREC>(w0);
+    const unsigned w1 = cvt_pk16<PREC>(r1, 0.f);           // mid
+    const float r2 = r1 - from16_lo<PREC>(w1);
+    const unsigned w2 = cvt_pk16<PREC>(r2, 0.f);           // lo
     return __builtin_bit_cast(bf16x8, u32x4{w0 | (w1 << 16), w2, 0u, 0u});
 }
 
-__device__ __forceinline__ bf16x8 bf16_ones() {
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = static_cast<__bf16>(1.0f);
-    return o;
+template <int PREC>
+__device__ __forceinline__ bf16x8 ones16() {
+    const unsigned one = PREC == NR_PREC_FP16 ? 0x3C003C00u : 0x3F803F80u;
+    return __builtin_bit_cast(bf16x8, u32x4{one, one, one, one});
 }
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
@@ -235,8 +272,8 @@ __device__ __forceinline__ unsigned nz_pk(unsigned w) {
 
 // fp32 accumulators (bias included) -> bf16 B operands; ReLU in fp32 when a VALU
 // head reads the same activations, else on the packed pairs; optional mask bits.
-template <int NBO, bool RELU, bool RELU_F32, bool MASK>
-__device__ __forceinline__ void epi_bf16(f32x16 (&acc)[NBO], bf16x8 (&out)[NBO][2], unsigned (&mw)[4]) {
+template <int PREC, int NBO, bool RELU, bool RELU_F32, bool MASK>
+__device__ __forceinline__ void epi16(f32x16 (&acc)[NBO], bf16x8 (&out)[NBO][2], unsigned (&mw)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) mw[q] = 0u;
 #pragma unroll
@@ -246,7 +283,7 @@ __device__ __forceinline__ void epi_bf16(f32x16 (&acc)[NBO], bf16x8 (&out)[NBO][
             for (int r = 0; r < 16; ++r) acc[nb][r] = __int_as_float(max(__float_as_int(acc[nb][r]), 0));
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
-            u32x4 wd = __builtin_bit_cast(u32x4, pack8(acc[nb], hf));
+            u32x4 wd = __builtin_bit_cast(u32x4, pack8<PREC>(acc[nb], hf));
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 if constexpr (RELU && !RELU_F32) wd[m] = relu_pk(wd[m]);
@@ -275,7 +312,7 @@ __device__ __forceinline__ void mask_pk(bf16x8 (&v)[2], unsigned word, int nb) {
 // (bf16: packed-pair mask words of epi_bf16; fp32: bit (nb&1)*16 + r of word nb>>1).
 template <int PREC>
 __device__ __forceinline__ void to_in_masked(f32x16 a, const u32x4& mw, int nb, InBlk<PREC>& o) {
-    if constexpr (PREC == NR_PREC_BF16) {
+    if constexpr (k16<PREC>) {
         to_in<PREC>(a, o);
         mask_pk(o.s, mw[nb >> 1], nb);
     } else {
@@ -294,7 +331,7 @@ __device__ __forceinline__ void store_img(char* __restrict__ region, int64_t til
                                           const InBlk<PREC>& v, int) {
     // wave-uniform base (tile is per wave) + the lane's 16 B: saddr + voffset stores
     char* base = region + ((tile * nblk + blk) * kFPB<PREC>) * static_cast<int64_t>(kFragBytes) + lane16();
-    if constexpr (PREC == NR_PREC_BF16) {
+    if constexpr (k16<PREC>) {
 #if NR_NT_STORE
         // streaming (non-temporal) stores: the 4 GB of images must not evict the
         // L2-resident weight stream every workgroup re-reads
@@ -316,7 +353,7 @@ template <int PREC>
 __device__ __forceinline__ void load_img(const char* __restrict__ region, int64_t tile, int nblk, int blk,
                                          InBlk<PREC>& v, int) {
     const char* base = region + ((tile * nblk + blk) * kFPB<PREC>) * static_cast<int64_t>(kFragBytes) + lane16();
-    if constexpr (PREC == NR_PREC_BF16) {
+    if constexpr (k16<PREC>) {
         v.s[0] = *reinterpret_cast<const bf16x8*>(base);
         v.s[1] = *reinterpret_cast<const bf16x8*>(base + kFragBytes);
     } else {
@@ -503,18 +540,18 @@ struct Act {
     __device__ __forceinline__ InBlk<PREC> operator()(int t, int kb) const { return v[t][kb]; }
     __device__ __forceinline__ void put(int t, int nb, const InBlk<PREC>& x) { v[t][nb] = x; }
 };
-template <int TPW, int NBLK>
-struct Act<NR_PREC_BF16, TPW, NBLK, true> {
+template <int PREC, int TPW, int NBLK>
+struct Act<PREC, TPW, NBLK, true> {
     char* base;  // the wave's region (wave-uniform)
     static constexpr int kBytes = TPW * NBLK * 2 * kFragBytes;
-    __device__ __forceinline__ InBlk<NR_PREC_BF16> operator()(int t, int kb) const {
+    __device__ __forceinline__ InBlk<PREC> operator()(int t, int kb) const {
         const char* p = base + lane16() + (t * NBLK + kb) * 2 * kFragBytes;
-        InBlk<NR_PREC_BF16> r;
+        InBlk<PREC> r;
         r.s[0] = *reinterpret_cast<const bf16x8*>(p);
         r.s[1] = *reinterpret_cast<const bf16x8*>(p + kFragBytes);
         return r;
     }
-    __device__ __forceinline__ void put(int t, int nb, const InBlk<NR_PREC_BF16>& x) {
+    __device__ __forceinline__ void put(int t, int nb, const InBlk<PREC>& x) {
         char* p = base + lane16() + (t * NBLK + nb) * 2 * kFragBytes;
         *reinterpret_cast<bf16x8*>(p) = x.s[0];
         *reinterpret_cast<bf16x8*>(p + kFragBytes) = x.s[1];
@@ -578,17 +615,17 @@ __device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1]
             const int r1 = r < N1 ? r : 0;
             const int r2 = r >= N1 ? (r - N1) % I2 : 0;
             (void)I1;
-            if constexpr (PREC == NR_PREC_BF16) {
+            if constexpr (k16<PREC>) {
                 const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(fp);
                 const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(fp + kFragBytes);
 #pragma unroll
                 for (int t = 0; t < TPW; ++t) {
                     if (r < N1) {
-                        acc1[t][r1] = mfma_bf16(a0, in[t].s[0], acc1[t][r1]);
-                        acc1[t][r1] = mfma_bf16(a1, in[t].s[1], acc1[t][r1]);
+                        acc1[t][r1] = mfma16<PREC>(a0, in[t].s[0], acc1[t][r1]);
+                        acc1[t][r1] = mfma16<PREC>(a1, in[t].s[1], acc1[t][r1]);
                     } else {
-                        acc2[t][r2] = mfma_bf16(a0, in[t].s[0], acc2[t][r2]);
-                        acc2[t][r2] = mfma_bf16(a1, in[t].s[1], acc2[t][r2]);
+                        acc2[t][r2] = mfma16<PREC>(a0, in[t].s[0], acc2[t][r2]);
+                        acc2[t][r2] = mfma16<PREC>(a1, in[t].s[1], acc2[t][r2]);
                     }
                 }
             } else {
@@ -678,7 +715,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     stream_begin(ring, st, a.packed, a.sd, tid);
 
     f32x16 acc[TPW][kHB];
-    constexpr bool ACT_LDS = PREC == NR_PREC_BF16 && NT == 512;
+    constexpr bool ACT_LDS = k16<PREC> && NT == 512;
     Act<PREC, TPW, kHB, ACT_LDS> hin;
     if constexpr (ACT_LDS)
         hin.base = lds + 2 * a.slot_bytes + wv * Act<PREC, TPW, kHB, ACT_LDS>::kBytes;
@@ -690,7 +727,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
         float bl[kHB];  // bf16: this layer's bias, lane < 32 holds rows 32 nb + lane
-        if constexpr (PREC == NR_PREC_BF16)
+        if constexpr (k16<PREC>)
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) bl[nb] = lane < 32 ? a.params[a.bo[i] + 32 * nb + lane] : 0.f;
         const bool skip_in = i > 0 && ((a.skips >> (i - 1)) & 1u);
@@ -720,7 +757,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                     f32x16 v;
 #pragma unroll
                     for (int r = 0; r < 16; ++r)
-                        v[r] = (PREC == NR_PREC_BF16 && NR_FASTPE)
+                        v[r] = (k16<PREC> && NR_FASTPE)
                                    ? pe_fast(pr, 32 * kb + acc_row(r, 0), 32 * kb + acc_row(r, 1), h != 0, a.L)
                                    : pe_feat(p0, p1, p2, 32 * kb + acc_row(r, h), a.L);
                     to_in<PREC>(v, xe.v[t][kb]);
@@ -735,16 +772,16 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                                                        sink_of(SV_H0 + i - 1, kHB));
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-            if constexpr (PREC == NR_PREC_BF16) {
+            if constexpr (k16<PREC>) {
                 bf16x8 hv[kHB][2];
                 if (NR_BIASMFMA) {
 #pragma unroll
-                    for (int nb = 0; nb < kHB; ++nb) acc[t][nb] = mfma_bf16(bias_frag(bl[nb]), bf16_ones(), acc[t][nb]);
+                    for (int nb = 0; nb < kHB; ++nb) acc[t][nb] = mfma16<PREC>(bias_frag<PREC>(bl[nb]), ones16<PREC>(), acc[t][nb]);
                 } else {
                     unsigned wt[4];
                     bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[i], lane), wt);
                 }
-                epi_bf16<kHB, true, false, TRAIN>(acc[t], hv, w);
+                epi16<PREC, kHB, true, false, TRAIN>(acc[t], hv, w);
 #pragma unroll
                 for (int nb = 0; nb < kHB; ++nb) hin.put(t, nb, InBlk<PREC>{{hv[nb][0], hv[nb][1]}});
             } else {
@@ -792,18 +829,18 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                                                sink_of(SV_H0 + n - 1, kHB));
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        if constexpr (PREC == NR_PREC_BF16) {
+        if constexpr (k16<PREC>) {
             bf16x8 hv[kHB][2];
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) {
                 const float b = lane < 32 ? a.params[a.bo[n] + 32 * nb + lane] : 0.f;
-                if (NR_BIASMFMA) acc[t][nb] = mfma_bf16(bias_frag(b), bf16_ones(), acc[t][nb]);
+                if (NR_BIASMFMA) acc[t][nb] = mfma16<PREC>(bias_frag<PREC>(b), ones16<PREC>(), acc[t][nb]);
             }
             if (!NR_BIASMFMA) {
                 unsigned wt[4];
                 bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[n], lane), wt);
             }
-            epi_bf16<kHB, false, false, false>(acc[t], hv, w);
+            epi16<PREC, kHB, false, false, false>(acc[t], hv, w);
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) hin.put(t, nb, InBlk<PREC>{{hv[nb][0], hv[nb][1]}});
         } else {
@@ -840,7 +877,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                 f32x16 v;
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
-                    v[r] = (PREC == NR_PREC_BF16 && NR_FASTPE)
+                    v[r] = (k16<PREC> && NR_FASTPE)
                                ? pe_fast(pr, 32 * kb + acc_row(r, 0), 32 * kb + acc_row(r, 1), h != 0, a.Ld)
                                : pe_feat(d0, d1, d2, 32 * kb + acc_row(r, h), a.Ld);
                 to_in<PREC>(v, de.v[t][kb]);
@@ -853,17 +890,17 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
         bf16x8 hcv[NC][2];
-        if constexpr (PREC == NR_PREC_BF16) {
+        if constexpr (k16<PREC>) {
 #pragma unroll
             for (int nb = 0; nb < NC; ++nb) {
                 const float b = lane < 32 ? a.params[a.bo[n + 1] + 32 * nb + lane] : 0.f;
-                if (NR_BIASMFMA) ac[t][nb] = mfma_bf16(bias_frag(b), bf16_ones(), ac[t][nb]);
+                if (NR_BIASMFMA) ac[t][nb] = mfma16<PREC>(bias_frag<PREC>(b), ones16<PREC>(), ac[t][nb]);
             }
             if (!NR_BIASMFMA) {
                 unsigned wt[4];
                 bias_act<NC, false>(ac[t], vimg(a.packed, a.vb[n + 1], lane), wt);
             }
-            epi_bf16<NC, true, true, TRAIN>(ac[t], hcv, w);
+            epi16<PREC, NC, true, true, TRAIN>(ac[t], hcv, w);
         } else {
             bias_act<NC, true>(ac[t], vimg(a.packed, a.vb[n + 1], lane), w);
         }
@@ -872,7 +909,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
 #pragma unroll
                 for (int nb = 0; nb < NC; ++nb) {
                     InBlk<PREC> v;
-                    if constexpr (PREC == NR_PREC_BF16)
+                    if constexpr (k16<PREC>)
                         v = InBlk<PREC>{{hcv[nb][0], hcv[nb][1]}};
                     else
                         to_in<PREC>(ac[t][nb], v);
@@ -908,6 +945,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
 
 // ----------------------------------------------------------- backward -----
 struct BwdArgs {
+    float gscale, inv_gscale;  // fp16 loss scale applied to dL/d(rgb, sigma); 1 otherwise
     const char* packed;
     const float* params;
     const float* x;
@@ -979,9 +1017,9 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const float y = a.rgb[3 * m + c];
-                dr[c] = (a.g_rgb[3 * m + c] * (1.0f - y)) * y;
+                dr[c] = ((a.g_rgb[3 * m + c] * (1.0f - y)) * y) * a.gscale;
             }
-            dzs[t] = a.sigma[m] > 0.f ? a.g_sigma[m] : 0.f;
+            dzs[t] = (a.sigma[m] > 0.f ? a.g_sigma[m] : 0.f) * a.gscale;
         }
         if (tok[t]) {
             // dz of the heads as one 32-feature block: feature 0 sigma, 1..3 rgb
@@ -1020,7 +1058,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
 
     // d [feat | d_enc] = W_dir^T dz_c   (feature_linear has no activation: dz_feat = d feat)
     f32x16 acc[TPW][kHB];
-    constexpr bool ACT_LDS = PREC == NR_PREC_BF16 && NT == 512;
+    constexpr bool ACT_LDS = k16<PREC> && NT == 512;
     Act<PREC, TPW, kHB, ACT_LDS> hin;
     if constexpr (ACT_LDS)
         hin.base = lds + 2 * a.slot_bytes + wv * Act<PREC, TPW, kHB, ACT_LDS>::kBytes;
@@ -1054,9 +1092,9 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
                 g1 += __shfl_xor(g1, 32);
                 g2 += __shfl_xor(g2, 32);
                 if (valid && h == 0) {
-                    a.g_d[3 * m] = g0;
-                    a.g_d[3 * m + 1] = g1;
-                    a.g_d[3 * m + 2] = g2;
+                    a.g_d[3 * m] = g0 * a.inv_gscale;
+                    a.g_d[3 * m + 1] = g1 * a.inv_gscale;
+                    a.g_d[3 * m + 2] = g2 * a.inv_gscale;
                 }
             }
         }
@@ -1162,9 +1200,9 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
                 g1 += __shfl_xor(g1, 32);
                 g2 += __shfl_xor(g2, 32);
                 if (valid && h == 0) {
-                    a.g_x[3 * m] = g0;
-                    a.g_x[3 * m + 1] = g1;
-                    a.g_x[3 * m + 2] = g2;
+                    a.g_x[3 * m] = g0 * a.inv_gscale;
+                    a.g_x[3 * m + 1] = g1 * a.inv_gscale;
+                    a.g_x[3 * m + 2] = g2 * a.inv_gscale;
                 }
             }
         }
@@ -1262,7 +1300,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     // per piece and tile made this kernel SALU-bound).
     const int total = (NBz + KB) * FPB;
     const int per_wave = (total + kDwWaves - 1) / kDwWaves;
-    constexpr int kMaxPW = PREC == NR_PREC_BF16 ? 6 : 10;
+    constexpr int kMaxPW = k16<PREC> ? 6 : 10;
     const char* psrc[kMaxPW];
     int64_t pstride[kMaxPW];
     int pdst[kMaxPW];  // LDS offset within a stage, or -1: scratch KB
@@ -1278,7 +1316,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
             int sg = 0, p0 = 0;
             while (pc >= p0 + a.seg_blocks[j][sg] * FPB) p0 += a.seg_blocks[j][sg++] * FPB;
             const int nb = a.seg_blocks[j][sg];
-            const int L = PREC == NR_PREC_BF16 ? dw_slot(lane, (pc - p0) % FPB) : lane;
+            const int L = k16<PREC> ? dw_slot(lane, (pc - p0) % FPB) : lane;
             pstride[k] = static_cast<int64_t>(nb) * BLK;
             psrc[k] = a.seg_ptr[j][sg] + t0 * pstride[k] + (pc - p0) * kFragBytes + L * 16;
             pdst[k] = pad ? -1 : pc * kFragBytes;
@@ -1316,9 +1354,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
         for (int q = 0; q < kDwQ; ++q) zero(acc[p][q]);
     float bsum[kDwP] = {0.f, 0.f, 0.f, 0.f};  // fp32 images
     f32x16 accb[kDwP];                        // bf16 images: D[row][*] = sum of dz[row]
-    bf16x8 ones;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) ones[e] = static_cast<__bf16>(1.0f);
+    const bf16x8 ones = ones16<PREC>();
 #pragma unroll
     for (int p = 0; p < kDwP; ++p) zero(accb[p]);
     bool nval[kDwP], kval[kDwQ];
@@ -1349,8 +1385,8 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
         bnext = bnext + 1 == NS ? 0 : bnext + 1;
         const char* buf = lds + bcur * a.stage_bytes;
         bcur = bcur + 1 == NS ? 0 : bcur + 1;
-        if (PREC == NR_PREC_BF16 || active) {
-            if constexpr (PREC == NR_PREC_BF16) {
+        if (k16<PREC> || active) {
+            if constexpr (k16<PREC>) {
                 const uint32_t bufA = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf)) + kDwP * nbg * BLK;
                 const uint32_t bufB = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf)) +
                                       (NBz + kDwQ * kbg) * BLK;
@@ -1382,11 +1418,11 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
                     // or return 0); per-MFMA validity branches made this loop SALU-bound
                     for (int p = 0; p < kDwP; ++p)
 #pragma unroll
-                        for (int q = 0; q < kDwQ; ++q) acc[p][q] = mfma_bf16(A[p], Bm[q], acc[p][q]);
+                        for (int q = 0; q < kDwQ; ++q) acc[p][q] = mfma16<PREC>(A[p], Bm[q], acc[p][q]);
                     // bias gradient = dz summed over samples: an MFMA against ones
                     if (do_bias)
 #pragma unroll
-                        for (int p = 0; p < kDwP; ++p) accb[p] = mfma_bf16(A[p], ones, accb[p]);
+                        for (int p = 0; p < kDwP; ++p) accb[p] = mfma16<PREC>(A[p], ones, accb[p]);
                 }
             } else {
                 // fp32 image [tq][L][4]: operand row r <-> (hh = r>>4, reg i = r&15 -> frag i>>2, elem i&3)
@@ -1436,7 +1472,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
             }
         }
         if (do_bias) {
-            if constexpr (PREC == NR_PREC_BF16) {
+            if constexpr (k16<PREC>) {
                 // every column of accb holds the row sums: lanes 0 and 32 (column 0) write them
                 if (ml == 0)
 #pragma unroll
@@ -1455,6 +1491,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
 struct ReduceArgs {
     const float* slabs;
     float* g;
+    float inv_gscale;  // fp16: undo the backward's loss scale (a power of two: exact)
     int64_t param_count;
     int chunks;
     int64_t slab_floats_per_chunk;
@@ -1497,7 +1534,7 @@ __global__ void mlp_dw_reduce_kernel(ReduceArgs a) {
     const float* s = a.slabs + a.job_slab[job] + row * ld + col;
     float acc = 0.f;
     for (int c = 0; c < a.chunks; ++c) acc += s[static_cast<int64_t>(c) * a.slab_floats_per_chunk];
-    a.g[pidx] = acc;
+    a.g[pidx] = acc * a.inv_gscale;
 }
 
 // ---------------------------------------------------------------- pack ----
@@ -1538,7 +1575,7 @@ __global__ void mlp_pack_kernel(PackArgs a) {
     int64_t e = g - a.cum[l];
     const bool bwd = e >= img;
     if (bwd) e -= img;
-    const bool bf = a.prec == NR_PREC_BF16;
+    const bool bf = a.prec != NR_PREC_FP32;  // 16-bit image (bf16 or fp16)
     const int epl = bf ? 8 : 4, fpb = bf ? 2 : 4;
     const int64_t frag = e / (64 * epl);
     const int lane = static_cast<int>((e / epl) % 64);
@@ -1561,7 +1598,8 @@ __global__ void mlp_pack_kernel(PackArgs a) {
     const float v = col >= 0 ? a.params[a.w_off[l] + static_cast<int64_t>(row) * a.in[l] + col] : 0.f;
     char* dst = a.packed + (bwd ? a.pkb[l] : a.pk[l]);
     if (bf)
-        reinterpret_cast<unsigned short*>(dst)[e] = bf16_bits(v);
+        reinterpret_cast<unsigned short*>(dst)[e] =
+            a.prec == NR_PREC_FP16 ? __builtin_bit_cast(unsigned short, static_cast<_Float16>(v)) : bf16_bits(v);
     else
         reinterpret_cast<float*>(dst)[e] = v;
 }
@@ -1709,15 +1747,15 @@ int max_chunk(const StreamDesc& sd) {
 
 template <int PREC, bool TRAIN>
 int launch_fwd(const MlpPlan& p, FwdArgs& a, hipStream_t s) {
-    constexpr int TPW = NR_FWD_TPW, NT = PREC == NR_PREC_BF16 ? NR_FWD_NT : 256;
-    constexpr int G = (PREC == NR_PREC_BF16 ? 16384 : 32768) / (NT * 16);  // one 16 / 32 KB chunk
+    constexpr int TPW = NR_FWD_TPW, NT = k16<PREC> ? NR_FWD_NT : 256;
+    constexpr int G = (k16<PREC> ? 16384 : 32768) / (NT * 16);  // one 16 / 32 KB chunk
     const int mc = max_chunk(a.sd);
     if (mc > G * NT * 16) {
         set_error("nr_mlp_forward: chunk of %d bytes exceeds the stager", mc);
         return NR_EARG;
     }
     a.slot_bytes = mc;
-    constexpr bool ACT_LDS = PREC == NR_PREC_BF16 && NT == 512;
+    constexpr bool ACT_LDS = k16<PREC> && NT == 512;
     const size_t lds = 2 * static_cast<size_t>(mc) + (ACT_LDS ? (NT / 64) * TPW * kHB * 2 * kFragBytes : 0);
     if (lds > 160 * 1024) {
         set_error("nr_mlp_forward: %zu bytes of LDS exceed 160 KiB", lds);
@@ -1743,16 +1781,16 @@ int launch_fwd(const MlpPlan& p, FwdArgs& a, hipStream_t s) {
 template <int PREC, bool WX>
 int launch_bwd(const MlpPlan& p, BwdArgs& a, hipStream_t s) {
     // the input-gradient variant also carries d x_enc through the trunk: 4 waves, 512 registers
-    constexpr int TPW = 1, NT = (WX || PREC != NR_PREC_BF16) ? 256 : NR_BWD_NT;
+    constexpr int TPW = 1, NT = (WX || !k16<PREC>) ? 256 : NR_BWD_NT;
     // one chunk of the skip layer's W^T: (XB + 8) blocks, at most 20 / 40 KB
-    constexpr int G = ((PREC == NR_PREC_BF16 ? 20480 : 40960) + NT * 16 - 1) / (NT * 16);
+    constexpr int G = ((k16<PREC> ? 20480 : 40960) + NT * 16 - 1) / (NT * 16);
     const int mc = max_chunk(a.sd);
     if (mc > G * NT * 16) {
         set_error("nr_mlp_backward_dx: chunk of %d bytes exceeds the stager", mc);
         return NR_EARG;
     }
     a.slot_bytes = mc;
-    constexpr bool ACT_LDS = PREC == NR_PREC_BF16 && NT == 512;
+    constexpr bool ACT_LDS = k16<PREC> && NT == 512;
     const size_t lds = 2 * static_cast<size_t>(mc) + (ACT_LDS ? (NT / 64) * TPW * kHB * 2 * kFragBytes : 0);
     if (lds > 160 * 1024) {
         set_error("nr_mlp_backward_dx: %zu bytes of LDS exceed 160 KiB", lds);
@@ -1935,6 +1973,8 @@ int nr_mlp_forward(const NrMlpConfig* cfg, const void* packed, const float* para
     const hipStream_t s = static_cast<hipStream_t>(stream);
     if (p.prec == NR_PREC_BF16)
         return saved ? launch_fwd<NR_PREC_BF16, true>(p, a, s) : launch_fwd<NR_PREC_BF16, false>(p, a, s);
+    if (p.prec == NR_PREC_FP16)
+        return saved ? launch_fwd<NR_PREC_FP16, true>(p, a, s) : launch_fwd<NR_PREC_FP16, false>(p, a, s);
     return saved ? launch_fwd<NR_PREC_FP32, true>(p, a, s) : launch_fwd<NR_PREC_FP32, false>(p, a, s);
 }
 
@@ -1955,6 +1995,8 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     BwdArgs b;
     std::memset(&b, 0, sizeof(b));
     b.packed = static_cast<const char*>(packed);
+    b.gscale = grad_scale(p.prec);
+    b.inv_gscale = 1.0f / b.gscale;
     b.params = params;
     b.x = x;
     b.d = d;
@@ -1995,6 +2037,8 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     b.ws_heads = p.ws_heads;
     if (p.prec == NR_PREC_BF16)
         return wx ? launch_bwd<NR_PREC_BF16, true>(p, b, s) : launch_bwd<NR_PREC_BF16, false>(p, b, s);
+    if (p.prec == NR_PREC_FP16)
+        return wx ? launch_bwd<NR_PREC_FP16, true>(p, b, s) : launch_bwd<NR_PREC_FP16, false>(p, b, s);
     return wx ? launch_bwd<NR_PREC_FP32, true>(p, b, s) : launch_bwd<NR_PREC_FP32, false>(p, b, s);
 }
 
@@ -2048,6 +2092,8 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
     const dim3 grid(static_cast<unsigned>(p.n_jobs * z.chunks)), block(kDwThreads);
     if (p.prec == NR_PREC_BF16)
         hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_BF16>, grid, block, lds, s, w);
+    else if (p.prec == NR_PREC_FP16)
+        hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_FP16>, grid, block, lds, s, w);
     else
         hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_FP32>, grid, block, lds, s, w);
     NR_LAUNCH_CHECK("nr_mlp_backward_dw");
@@ -2069,6 +2115,7 @@ int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M, const void* worksp
     std::memset(&r, 0, sizeof(r));
     r.slabs = reinterpret_cast<const float*>(static_cast<const char*>(workspace) + z.slab_off);
     r.g = g_params;
+    r.inv_gscale = 1.0f / grad_scale(p.prec);
     r.param_count = p.param_count;
     r.chunks = z.chunks;
     r.slab_floats_per_chunk = p.slab_floats_per_chunk;

@@ -45,6 +45,7 @@ class NrMlpConfig(ctypes.Structure):
 
 NR_PREC_FP32 = 0
 NR_PREC_BF16 = 1
+NR_PREC_FP16 = 2
 _cfg_p = ctypes.POINTER(NrMlpConfig)
 
 # name -> (restype, argtypes); mirrors include/nerf_hip.h one to one.

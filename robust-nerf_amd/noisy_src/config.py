@@ -6,8 +6,10 @@ Every reference field keeps its name and default, so ``NeRFConfig()`` and the
 reference's CLI-built configs mean the same thing here.  The MI355X build adds
 only defaulted fields:
 
-* ``ModelConfig.precision`` — ``"fp32"`` (exact fp32 MFMA, the parity mode) or
-  ``"bf16"`` (bf16 MFMA operands, fp32 accumulation and fp32 master weights);
+* ``ModelConfig.precision`` — ``"fp32"`` (exact fp32 MFMA, the parity mode),
+  ``"bf16"`` (bf16 MFMA operands, fp32 accumulation and fp32 master weights) or
+  ``"fp16"`` (BASELINE cfg #5: fp16 operands, fp32 accumulation, backward on dz
+  scaled by 2^14);
 * ``TrainConfig.world_size`` / ``TrainConfig.global_batch`` — ray-batch data
   parallelism over RCCL (one process per GPU).
 """

@@ -57,7 +57,9 @@ def _precision_code(p: str) -> int:
         return _hip.NR_PREC_FP32
     if p == "bf16":
         return _hip.NR_PREC_BF16
-    raise ValueError(f"ModelConfig.precision must be 'fp32' or 'bf16', got {p!r}")
+    if p == "fp16":
+        return _hip.NR_PREC_FP16
+    raise ValueError(f"ModelConfig.precision must be 'fp32', 'bf16' or 'fp16', got {p!r}")
 
 
 class _MLPFunction(torch.autograd.Function):

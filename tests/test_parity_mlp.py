@@ -132,6 +132,37 @@ def test_bf16_forward_backward():
         assert rel < 1e-2, (name, rel)
 
 
+def test_fp16_forward_backward():
+    """fp16 MFMA path (BASELINE cfg #5) vs the oracle with fp16-rounded operands.  The
+    backward runs on dz scaled by 2^14 (undone exactly in the dW reduce); upstream
+    gradients have the magnitude of a mean loss over 4096 rays."""
+    oracle, net = _pair("fp16")
+    emu = ref.fp16_operand_nerf(oracle)
+    x, d = _inputs(1500)
+    with torch.no_grad():
+        rgb, sig = net(x.to(DEV), d.to(DEV))
+        er, es = emu(x, d)
+        wr, ws = oracle(x, d)
+    assert (rgb.cpu() - er).abs().max() < 1e-4
+    assert (sig.cpu() - es).abs().max() < 1e-4
+    assert (rgb.cpu() - wr).abs().max() < 1e-3  # vs fp32: fp16 operand rounding
+    keep = _kink_free(oracle, x, d, eps=1e-3).float()[:, None]
+    g = torch.Generator().manual_seed(3)
+    scale = 2.0 / (3 * 4096)
+    gr = torch.randn(1500, 3, generator=g) * keep * scale
+    gs = torch.randn(1500, 1, generator=g) * keep * scale
+    er, es = emu(x, d)
+    ((er * gr).sum() + (es * gs).sum()).backward()
+    rgb, sig = net(x.to(DEV), d.to(DEV))
+    ((rgb * gr.to(DEV)).sum() + (sig * gs.to(DEV)).sum()).backward()
+    for (name, pe), pg in zip(emu.named_parameters(), net.parameters()):
+        a, b = pg.grad.cpu(), pe.grad
+        assert torch.isfinite(a).all(), name
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        # dz is stored in fp16 for the dW GEMM: <= ~1 fp16 ulp (2^-11)
+        assert rel < 3e-3, (name, rel)
+
+
 def test_no_view_dirs_and_other_skips():
     oracle, net = _pair("fp32", skips=(2,), use_view_dirs=False)
     x, _ = _inputs(300)
