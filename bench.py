@@ -10,7 +10,10 @@ poses of the reference's outputs/*/final_poses.pt fixture), 4096 rays per GPU
 per step (weak scaling), bf16 MFMA MLP with fp32 master weights.  The scene
 content is synthetic (random targets): the lego dataset is not available here.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision bf16|fp32]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision bf16|fp16|fp32]
+                    [--num-samples 64 --num-samples-fine 128]
+
+(BASELINE cfg #5 is --precision fp16 --num-samples 128 --num-samples-fine 256.)
 
 For N > 1 the driver runs it under torch.distributed.run (one rank per GPU).
 Rank 0 prints ONE JSON line.
@@ -34,7 +37,7 @@ import torch  # noqa: E402
 
 METRIC = "training rays/sec + test PSNR, lego 800² 64c+128f, at 1/2/4/8 MI355X"
 MACS_PER_EVAL = 593_408  # MLP multiply-adds per sample (forward)
-PEAK_TFLOPS = {"bf16": 2516.6, "fp32": 157.3}  # dense MFMA (256 CU x 2.4 GHz); MI355X_MICROARCH.md
+PEAK_TFLOPS = {"bf16": 2516.6, "fp16": 2516.6, "fp32": 157.3}  # dense MFMA (256 CU x 2.4 GHz); MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0  # HBM3E spec peak; MI355X_MICROARCH.md (~6300 achievable)
 
 # Algorithmic work per sample of each fused-MLP kernel (default 8x256 model, L=10/4):
@@ -62,7 +65,7 @@ def traffic_of(kernel: str, M: int, prec: str):
 
 def roofline_of(entry: str, M: int, ms: float, prec: str, n_params: int):
     """(bound, achieved, peak, unit, work-per-launch description) of one fused-MLP launch."""
-    esize = 2 if prec == "bf16" else 4
+    esize = 4 if prec == "fp32" else 2
     if entry == "nr_mlp_forward":
         return "mfma", 2.0 * MACS_PER_EVAL * M / (ms * 1e-3) / 1e12, PEAK_TFLOPS[prec], "TFLOP/s", \
             f"2 x {MACS_PER_EVAL} MAC x {M} samples"
@@ -123,7 +126,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=4096, help="rays per GPU per step")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--num-samples", type=int, default=64)
+    ap.add_argument("--num-samples-fine", type=int, default=128)
     ap.add_argument("--cpu-rays", type=int, default=1024)
     ap.add_argument("--cpu-steps", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -148,7 +153,7 @@ def main():
     torch.manual_seed(42)  # train.py:319 set_seed(42); identical init on every rank
     mc, mf = create_nerf(ModelConfig(precision=args.precision))
     mc, mf = mc.to(dev), mf.to(dev)
-    rcfg = RenderConfig()
+    rcfg = RenderConfig(num_samples=args.num_samples, num_samples_fine=args.num_samples_fine)
     trainer = Trainer(mc, mf, rcfg, process_group=pg)
 
     B = args.batch
@@ -203,7 +208,8 @@ def main():
         "dtype": args.precision,
         "data": "synthetic (lego 800x800 camera rays from the reference's GT poses; random targets)",
         "config": {
-            "workload": "lego 800x800 hierarchical 64c+128f training step, 4096 rays per GPU",
+            "workload": f"lego 800x800 hierarchical {rcfg.num_samples}c+{rcfg.num_samples_fine}f training step, "
+                        f"{B} rays per GPU",
             "global_batch": world * B,
             "num_samples": rcfg.num_samples,
             "num_samples_fine": rcfg.num_samples_fine,
@@ -226,6 +232,7 @@ def main():
                                 / (world * PEAK_TFLOPS[args.precision] * 1e12), 4),
         "kernel_ms": {k: round(v[1], 4) for k, v in calls.items()},
         "final_loss": round(loss, 6),
+        # test PSNR needs the lego test split (not available offline)
         "psnr": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
