@@ -1604,82 +1604,6 @@ __global__ void mlp_pack_kernel(PackArgs a) {
         reinterpret_cast<float*>(dst)[e] = v;
 }
 
-// Fast bf16 forward stream and bias fragments (mlp_plan.hpp FastUnit).  One thread
-// per bf16 element: stream element e = ((((u * 8 + pair) * 2 + s) * 64 + lane) * 8 + j)
-// holds A[i = lane & 31][k = 16 s + 8 (j >> 2) + 4 h + (j & 3)] of the pair's block
-// (the accumulator-order k permutation of the other images).  Bias fragments:
-// lane i < 32 of row block nb holds bias[32 nb + i] split as hi + mid + lo (bf16) in
-// elements 0..2; the kernel multiplies them by an all-ones B operand.
-struct PackFastArgs {
-    const float* params;
-    char* packed;
-    int n_fast;
-    FastUnit fast[kMaxFastUnits];
-    int64_t pk_fast;
-    int n_lin;
-    int64_t w_off[kMaxMfmaLayers], b_off[kMaxMfmaLayers], biasf[kMaxMfmaLayers];
-    int in[kMaxMfmaLayers], out[kMaxMfmaLayers], NB[kMaxMfmaLayers], nseg[kMaxMfmaLayers];
-    int seg_col0[kMaxMfmaLayers][kMaxSeg], seg_w[kMaxMfmaLayers][kMaxSeg], seg_blk[kMaxMfmaLayers][kMaxSeg];
-    int64_t sig_w, rgb_w;
-    int64_t n_stream, n_total;  // bf16 elements: stream, stream + bias fragments
-    int64_t bcum[kMaxMfmaLayers + 1];
-};
-
-__device__ __forceinline__ int fast_col(const PackFastArgs& a, int l, int kb, int c) {
-    int blk0 = 0;
-    for (int s = 0; s < a.nseg[l]; ++s) {
-        if (kb < blk0 + a.seg_blk[l][s]) {
-            const int cs = 32 * (kb - blk0) + c;
-            return cs < a.seg_w[l][s] ? a.seg_col0[l][s] + cs : -1;
-        }
-        blk0 += a.seg_blk[l][s];
-    }
-    return -1;
-}
-
-__global__ void mlp_pack_fast_kernel(PackFastArgs a) {
-    const int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (g >= a.n_total) return;
-    float v = 0.f;
-    if (g < a.n_stream) {
-        const int j = static_cast<int>(g & 7), lane = static_cast<int>((g >> 3) & 63);
-        const int sf = static_cast<int>((g >> 9) & 1), pair = static_cast<int>((g >> 10) & 7);
-        const int u = static_cast<int>(g >> 13);
-        const int i = lane & 31, h = lane >> 5;
-        const int kk = 16 * sf + 8 * (j >> 2) + 4 * h + (j & 3);
-        const FastUnit fu = a.fast[u];
-        if (fu.kind == FU_W) {
-            const int l = fu.layer, nb = a.NB[l];
-            if (pair < fu.nkb * nb) {
-                const int kb = fu.kb0 + pair / nb, row = 32 * (pair % nb) + i;
-                const int col = fast_col(a, l, kb, kk);
-                if (col >= 0 && row < a.out[l]) v = a.params[a.w_off[l] + static_cast<int64_t>(row) * a.in[l] + col];
-            }
-        } else if (fu.kind == FU_SIG) {
-            if (i == 0) v = a.params[a.sig_w + 32 * pair + kk];
-        } else if (pair < 4 && i < 3) {
-            v = a.params[a.rgb_w + i * (kHidden / 2) + 32 * pair + kk];
-        }
-        reinterpret_cast<unsigned short*>(a.packed + a.pk_fast)[g] = bf16_bits(v);
-        return;
-    }
-    const int64_t e = g - a.n_stream;
-    int l = 0;
-    while (e >= a.bcum[l + 1]) ++l;
-    const int64_t le = e - a.bcum[l];
-    const int j = static_cast<int>(le & 7), lane = static_cast<int>((le >> 3) & 63);
-    const int nb = static_cast<int>(le >> 9);
-    const int row = 32 * nb + (lane & 31);
-    if (lane < 32 && j < 3 && row < a.out[l]) {
-        const float b = a.params[a.b_off[l] + row];
-        const float hi = static_cast<float>(static_cast<__bf16>(b));
-        const float mid = static_cast<float>(static_cast<__bf16>(b - hi));
-        const float lo = static_cast<float>(static_cast<__bf16>((b - hi) - mid));
-        v = j == 0 ? hi : (j == 1 ? mid : lo);
-    }
-    reinterpret_cast<unsigned short*>(a.packed + a.biasf[l])[le] = bf16_bits(v);
-}
-
 // Vector images: element idx of a vector of NB blocks <-> feature 32*(idx>>5) + acc_row(idx&15, (idx>>4)&1).
 struct PackVecArgs {
     const float* params;
@@ -1730,7 +1654,9 @@ bool plan_or_error(const NrMlpConfig* cfg, MlpPlan* p) {
 #ifndef NR_BWD_NT
 #define NR_BWD_NT 512
 #endif
+#ifndef NR_FWD_TPW
 #define NR_FWD_TPW 1
+#endif
 
 void add_stream_layer(StreamDesc& sd, int nchunks, int chunk_kb, int load_kb = -1) {
     for (int c = 0; c < nchunks && sd.nq < kMaxChunks; ++c) {
@@ -1891,40 +1817,6 @@ int nr_mlp_pack(const NrMlpConfig* cfg, const float* params, void* packed, nr_st
         add_vec(p.rgb_w + c * (kHidden / 2), kHidden / 2, p.vrgb + c * (kHidden / 2) * 4, kHB / 2, 1);
     hipLaunchKernelGGL(mlp_pack_vec_kernel, dim3(ceil_div(v.cum[v.nv], 256)), dim3(256), 0, s, v);
     NR_LAUNCH_CHECK("nr_mlp_pack");
-    if (p.fast_ok) {
-        static PackFastArgs f;  // large (unit table): static, filled per call
-        std::memset(&f, 0, sizeof(f));
-        f.params = params;
-        f.packed = static_cast<char*>(packed);
-        f.n_fast = p.n_fast;
-        for (int u = 0; u < p.n_fast; ++u) f.fast[u] = p.fast[u];
-        f.pk_fast = p.pk_fast;
-        f.n_lin = p.n_lin;
-        f.bcum[0] = 0;
-        for (int l = 0; l < p.n_lin; ++l) {
-            const LinearDesc& d = p.lin[l];
-            f.w_off[l] = d.w_off;
-            f.b_off[l] = d.b_off;
-            f.biasf[l] = p.pk_biasf[l];
-            f.in[l] = d.in;
-            f.out[l] = d.out;
-            f.NB[l] = d.NB;
-            f.nseg[l] = d.nseg;
-            for (int q = 0; q < d.nseg; ++q) {
-                f.seg_col0[l][q] = d.seg[q].col0;
-                f.seg_w[l][q] = d.seg[q].width;
-                f.seg_blk[l][q] = d.seg[q].blocks;
-            }
-            f.bcum[l + 1] = f.bcum[l] + static_cast<int64_t>(d.NB) * 512;
-        }
-        f.sig_w = p.sig_w;
-        f.rgb_w = p.rgb_w;
-        f.n_stream = static_cast<int64_t>(p.n_fast) * (kFastUnitBytes / 2);
-        f.n_total = f.n_stream + f.bcum[p.n_lin];
-        hipLaunchKernelGGL(mlp_pack_fast_kernel, dim3(static_cast<unsigned>(ceil_div_ll(f.n_total, 256))), dim3(256), 0,
-                           s, f);
-        NR_LAUNCH_CHECK("nr_mlp_pack");
-    }
     return NR_OK;
 }
 

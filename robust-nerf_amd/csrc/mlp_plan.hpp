@@ -82,17 +82,6 @@ struct ReduceRange {
     int bjob, brow0;
 };
 
-// One 16-KB unit of the fast bf16 forward stream: 8 fragment pairs (2 KB each).
-// kind W: pair p = row block (p % nb) of k block kb0 + p / nb of layer `layer`
-// (2 k blocks per unit when nb = 4); SIG: pair p = k block p of w_sigma (row 0 of
-// a 32-row block); RGB: pair p < 4 = k block p of W_rgb (rows 0..2).
-enum FastUnitKind { FU_W = 0, FU_SIG = 1, FU_RGB = 2 };
-struct FastUnit {
-    int kind, layer, kb0, nkb;
-};
-constexpr int kMaxFastUnits = 200;
-constexpr int kFastUnitBytes = 16384;
-
 struct MlpPlan {
     int L, Ld, n_layers, use_vd, prec;
     uint32_t skips;
@@ -102,13 +91,6 @@ struct MlpPlan {
     LinearDesc lin[kMaxMfmaLayers];   // [0, n_layers) trunk, n_layers feat, n_layers+1 dir
     int64_t sig_w, sig_b, rgb_w, rgb_b;
     int64_t packed_bytes;
-    // fast bf16 forward (default model shape only; fast_ok): its unit stream and
-    // per-layer bias fragments (NB x 1 KB: bias split hi+mid+lo in bf16 at k = 0..2)
-    int fast_ok;
-    int n_fast;
-    FastUnit fast[kMaxFastUnits];
-    int64_t pk_fast;                  // byte offset of the unit stream (+1 zero unit of slack)
-    int64_t pk_biasf[kMaxMfmaLayers]; // byte offsets of the bias fragment images
     int64_t vsig, vrgb;               // byte offsets of the w_sigma / W_rgb vector images
     int esize;                        // bytes per saved/workspace element (2 bf16, 4 fp32)
     int fpb;                          // 1-KB fragments per 32x32 block (2 bf16, 4 fp32)

@@ -24,14 +24,29 @@ __device__ __forceinline__ float linspace01(int n, int i) {
 
 // Build cdf[0..nb-1] from wbuf[0..nb-2] (raw weights, +1e-5 applied here).
 // Every lane runs the same sequential recurrence; the owner lane stores.
-__device__ __forceinline__ void build_cdf(const float* wbuf, float* cdf, int nb, int lane) {
+// The divisions pdf_k = w_k / sum run in parallel (written over wbuf); the serial
+// chain is the cumsum alone (the caller syncs the workgroup before reading cdf).
+__device__ __forceinline__ void build_cdf(float* wbuf, float* cdf, int nb, int lane) {
     const int nw = nb - 1;
     float sum = 0.f;
     for (int k = 0; k < nw; ++k) sum += wbuf[k] + 1e-5f;
+    float pdf[8];  // nw <= 512 (64 lanes x 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = lane + 64 * j;
+        pdf[j] = k < nw ? (wbuf[k] + 1e-5f) / sum : 0.f;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = lane + 64 * j;
+        if (k < nw) wbuf[k] = pdf[j];
+    }
+    __builtin_amdgcn_wave_barrier();
     float run = 0.f;
     if (lane == 0) cdf[0] = 0.f;
     for (int k = 0; k < nw; ++k) {
-        run += (wbuf[k] + 1e-5f) / sum;
+        run += wbuf[k];
         if (((k + 1) & 63) == lane) cdf[k + 1] = run;
     }
 }
@@ -79,6 +94,7 @@ __global__ void sample_pdf_kernel(const float* bins_g, const float* w_g, const f
     }
 }
 
+template <int KP>  // ceil((Nc + Nf) / 64): sort entries per lane
 __global__ void sample_hier_kernel(const float* ro, const float* rd, const float* zc_g, const float* wc_g,
                                    const float* u_g, int B, int Nc, int Nf, float* zf_out, float* pts_out) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -110,10 +126,10 @@ __global__ void sample_hier_kernel(const float* ro, const float* rd, const float
     __syncthreads();
     if (!live) return;
     // all-pairs rank sort of uni[0..T): rank = #{q: x_q < x} + #{q < e: x_q == x}
-    float v[kMaxPerLane];
-    int rank[kMaxPerLane];
+    float v[KP];
+    int rank[KP];
 #pragma unroll
-    for (int k = 0; k < kMaxPerLane; ++k) {
+    for (int k = 0; k < KP; ++k) {
         const int e = lane + 64 * k;
         v[k] = e < T ? uni[e] : 0.f;
         rank[k] = 0;
@@ -121,7 +137,7 @@ __global__ void sample_hier_kernel(const float* ro, const float* rd, const float
     for (int q = 0; q < T; ++q) {
         const float x = uni[q];
 #pragma unroll
-        for (int k = 0; k < kMaxPerLane; ++k) {
+        for (int k = 0; k < KP; ++k) {
             const int e = lane + 64 * k;
             rank[k] += (x < v[k]) || (x == v[k] && q < e);
         }
@@ -133,7 +149,7 @@ __global__ void sample_hier_kernel(const float* ro, const float* rd, const float
         dx = rd[3 * b], dy = rd[3 * b + 1], dz = rd[3 * b + 2];
     }
 #pragma unroll
-    for (int k = 0; k < kMaxPerLane; ++k) {
+    for (int k = 0; k < KP; ++k) {
         const int e = lane + 64 * k;
         if (e < T) {
             const int64_t o = ob + rank[k];
@@ -158,7 +174,7 @@ int nr_sample_pdf(const float* bins, const float* weights, const float* u, int B
     NR_REQUIRE(bins && weights && samples && B >= 0 && Nb >= 2 && Ns > 0, "nr_sample_pdf: bad arguments");
     if (B == 0) return NR_OK;
     const size_t lds = sizeof(float) * kRaysPerBlock * 3 * Nb;
-    NR_REQUIRE(lds <= 64 * 1024, "nr_sample_pdf: Nb=%d too large", Nb);
+    NR_REQUIRE(lds <= 64 * 1024 && Nb - 1 <= 512, "nr_sample_pdf: Nb=%d too large", Nb);
     hipLaunchKernelGGL(sample_pdf_kernel, dim3(ceil_div(B, kRaysPerBlock)), dim3(64 * kRaysPerBlock), lds,
                        static_cast<hipStream_t>(stream), bins, weights, u, B, Nb, Ns, samples);
     NR_LAUNCH_CHECK("nr_sample_pdf");
@@ -173,8 +189,14 @@ int nr_sample_hierarchical(const float* ro, const float* rd, const float* zc, co
                64 * kMaxPerLane);
     if (B == 0) return NR_OK;
     const size_t lds = sizeof(float) * kRaysPerBlock * (3 * (Nc - 1) + Nc + Nf);
-    hipLaunchKernelGGL(sample_hier_kernel, dim3(ceil_div(B, kRaysPerBlock)), dim3(64 * kRaysPerBlock), lds,
-                       static_cast<hipStream_t>(stream), ro, rd, zc, wc, u, B, Nc, Nf, zf, pts);
+    const dim3 grid(ceil_div(B, kRaysPerBlock)), block(64 * kRaysPerBlock);
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    switch ((Nc + Nf + 63) / 64) {
+#define NR_HIER(K) \
+    case K: hipLaunchKernelGGL(sample_hier_kernel<K>, grid, block, lds, st, ro, rd, zc, wc, u, B, Nc, Nf, zf, pts); break;
+        NR_HIER(1) NR_HIER(2) NR_HIER(3) NR_HIER(4) NR_HIER(5) NR_HIER(6) NR_HIER(7) NR_HIER(8)
+#undef NR_HIER
+    }
     NR_LAUNCH_CHECK("nr_sample_hierarchical");
     return NR_OK;
 }
