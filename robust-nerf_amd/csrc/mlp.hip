@@ -175,6 +175,9 @@ __device__ __forceinline__ void pe_feat_bwd(float x0, float x1, float x2, int f,
 // fract(2^k hi) + 2^k lo (2^k hi exact).  Absolute error ~1e-6, far below the
 // bf16 rounding (2^-9 relative) the encoding goes through; the fp32 path keeps
 // sinf/cosf.  cos(v) = sin(v + 1/4 revolution).
+#ifndef NR_DW_CHUNK_MAJOR
+#define NR_DW_CHUNK_MAJOR 1
+#endif
 #ifndef NR_NT_STORE
 #define NR_NT_STORE 1
 #endif
@@ -1224,6 +1227,7 @@ constexpr int kDwP = 4, kDwQ = 2;  // blocks per wave: dz rows x input cols
 
 struct DwArgs {
     float* slabs;
+    int njobs;
     int64_t tiles;
     int tiles_per_chunk, chunks;
     int stage_bytes, nstage;
@@ -1280,7 +1284,13 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar staging loop
+#if NR_DW_CHUNK_MAJOR
+    // chunk-major: every job of a chunk runs at about the same time, so an input two
+    // jobs share (h_{n-1}: feature and heads jobs) is re-read from L2/MALL, not HBM
+    const int j = blockIdx.x % a.njobs, chunk = blockIdx.x / a.njobs;
+#else
     const int j = blockIdx.x / a.chunks, chunk = blockIdx.x % a.chunks;
+#endif
     const int NBz = a.job_NBz[j], KB = a.job_KB[j];
     const bool active = wv < a.job_waves[j];
     const int nbg = active ? wv % a.job_nbg[j] : 0, kbg = active ? wv / a.job_nbg[j] : 0;
@@ -1950,6 +1960,7 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
     w.slabs = reinterpret_cast<float*>(ws + z.slab_off);
     w.tiles = z.tiles;
     w.chunks = z.chunks;
+    w.njobs = p.n_jobs;
     w.tiles_per_chunk = static_cast<int>(ceil_div_ll(z.tiles, z.chunks));
     w.slab_floats_per_chunk = p.slab_floats_per_chunk;
     int max_blk = 0;
