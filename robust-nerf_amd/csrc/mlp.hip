@@ -175,6 +175,18 @@ __device__ __forceinline__ void pe_feat_bwd(float x0, float x1, float x2, int f,
 // fract(2^k hi) + 2^k lo (2^k hi exact).  Absolute error ~1e-6, far below the
 // bf16 rounding (2^-9 relative) the encoding goes through; the fp32 path keeps
 // sinf/cosf.  cos(v) = sin(v + 1/4 revolution).
+#ifndef NR_EPI_HOOK
+#define NR_EPI_HOOK 1  // 16-bit: layer epilogue overlapped with the last chunk's MFMAs
+#endif
+#ifndef NR_APF
+#define NR_APF 3  // 16-bit weight-stream A fragments read ahead (row blocks)
+#endif
+#ifndef NR_AB_NODMA
+#define NR_AB_NODMA 0  // A/B timing only (wrong results): no weight-stream DMA
+#endif
+#ifndef NR_AB_NOBAR
+#define NR_AB_NOBAR 0  // A/B timing only (racy): no stream barrier
+#endif
 #ifndef NR_DW_CHUNK_MAJOR
 #define NR_DW_CHUNK_MAJOR 1
 #endif
@@ -486,14 +498,19 @@ struct Stager {
     // barrier that publishes it is preceded by vmcnt(0).
     __device__ __forceinline__ void load(Ring& ring, const StreamDesc& sd, int q, int tid) {
         if (q >= sd.nq) return;
-        const int bytes = sd.ckb[q] * 1024;
+        load_sized(ring, q, sd.ckb[q], sd.cadv[q], tid);
+    }
+    // chunk q of ckb KB (advance cadv KB): sizes from the caller, no scalar loads
+    __device__ __forceinline__ void load_sized(Ring& ring, int q, int ckb, int cadv, int) {
+        if (NR_AB_NODMA) return;
+        const int bytes = ckb * 1024;
         char* slot = ring.lds + (q & 1) * ring.slot_bytes;
         const uint32_t l16 = lane16();
         for (int pc = ring.wv; pc * 1024 < bytes; pc += NT / 64)
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(ring.src + pc * 1024 + l16),
                 (__attribute__((address_space(3))) void*)(slot + pc * 1024), 16, 0, 0);
-        ring.src += sd.cadv[q] * 1024;
+        ring.src += cadv * 1024;
     }
 
     // Wait for this wave's pieces of the next chunk only: the `after` vector-memory
@@ -513,13 +530,16 @@ struct Stager {
 
     __device__ __forceinline__ void load(Ring& ring, const StreamDesc& sd, int q, int tid) {
         if (q >= sd.nq) return;
-        const int bytes = sd.ckb[q] * 1024;
+        load_sized(ring, q, sd.ckb[q], sd.cadv[q], tid);
+    }
+    __device__ __forceinline__ void load_sized(Ring& ring, int, int ckb, int cadv, int tid) {
+        const int bytes = ckb * 1024;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int b = (g * NT + tid) * 16;
             if (b < bytes) v[g] = *reinterpret_cast<const u32x4*>(ring.src + b);
         }
-        ring.src += sd.cadv[q] * 1024;
+        ring.src += cadv * 1024;
     }
 
     __device__ __forceinline__ void store(char* slot, const StreamDesc& sd, int q, int tid, int = 0) {
@@ -539,13 +559,20 @@ struct Stager {
 // the 64 registers that let two waves share a SIMD without spilling).
 template <int PREC, int TPW, int NBLK, bool LDS>
 struct Act {
+    static constexpr bool kLds = false;
     InBlk<PREC> v[TPW][NBLK];
     __device__ __forceinline__ InBlk<PREC> operator()(int t, int kb) const { return v[t][kb]; }
     __device__ __forceinline__ void put(int t, int nb, const InBlk<PREC>& x) { v[t][nb] = x; }
 };
 template <int PREC, int TPW, int NBLK>
 struct Act<PREC, TPW, NBLK, true> {
+    static constexpr bool kLds = true;
     char* base;  // the wave's region (wave-uniform)
+    // LDS byte address of this lane's 16 B of block kb of tile t (first fragment)
+    __device__ __forceinline__ uint32_t addr(int t, int kb) const {
+        return static_cast<uint32_t>(reinterpret_cast<uintptr_t>(base)) + lane16() +
+               static_cast<uint32_t>((t * NBLK + kb) * 2 * kFragBytes);
+    }
     static constexpr int kBytes = TPW * NBLK * 2 * kFragBytes;
     __device__ __forceinline__ InBlk<PREC> operator()(int t, int kb) const {
         const char* p = base + lane16() + (t * NBLK + kb) * 2 * kFragBytes;
@@ -586,30 +613,120 @@ struct Sink {
 // stager's counted vmcnt.
 __device__ __forceinline__ void stream_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!NR_AB_NOBAR) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
+
+// ds_read_b128 of the two 1-KB fragments of one 32x32 16-bit block (inline asm:
+// see stream_gemm) and the counted wait that publishes them.
+__device__ __forceinline__ void ds_read_pair(bf16x8 (&dst)[2], uint32_t addr) {
+    asm volatile("ds_read_b128 %0, %1" : "=v"(dst[0]) : "v"(addr));
+    asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(dst[1]) : "v"(addr));
+}
+// wait until at most n LDS/SMEM ops are outstanding (n: the reads issued after
+// these two, all younger LDS reads; SMEM only ever makes this wait longer)
+__device__ __forceinline__ void lgkm_wait_pair(int n, bf16x8& a0, bf16x8& a1) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0), "+v"(a1)); break;
+        case 2: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a0), "+v"(a1)); break;
+        case 4: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a0), "+v"(a1)); break;
+        case 6: asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a0), "+v"(a1)); break;
+        default: asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(a0), "+v"(a1)); break;
+    }
+}
+
+// Epilogue hooks of stream_gemm's last chunk (16-bit, one tile per wave): as the
+// MFMAs of row block r issue, the bias MFMA of block r-1 and the packing / ReLU /
+// mask bits / LDS store of block r-2 run, so the layer epilogue overlaps the
+// matrix pipe instead of following it with every wave of the workgroup idle.
+struct NoEpi {
+    static constexpr bool kOn = false;
+    __device__ __forceinline__ void bias(int) const {}
+    __device__ __forceinline__ void finish(int) const {}
+};
+
+template <int PREC, bool RELU, bool MASK>
+__device__ __forceinline__ void epi16_blk(const f32x16& a, bf16x8 (&out)[2], unsigned* mw, int nb) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+        u32x4 wd = __builtin_bit_cast(u32x4, pack8<PREC>(a, hf));
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            if constexpr (RELU) wd[m] = relu_pk(wd[m]);
+            if constexpr (MASK) mw[nb >> 1] |= nz_pk(wd[m]) << (8 * (nb & 1) + 4 * hf + m);
+        }
+        out[hf] = __builtin_bit_cast(bf16x8, wd);
+    }
+}
+
+template <int PREC, bool RELU, bool MASK, class Dst>
+struct LayerEpi {
+    static constexpr bool kOn = true;
+    f32x16* acc;      // the layer's accumulators (one tile)
+    const float* bl;  // bias, lane < 32 holds row 32 nb + lane
+    Dst* dst;         // where the 16-bit output blocks go (LDS activations)
+    unsigned* mw;     // mask words (MASK)
+    __device__ __forceinline__ void bias(int nb) const {
+        acc[nb] = mfma16<PREC>(bias_frag<PREC>(bl[nb]), ones16<PREC>(), acc[nb]);
+    }
+    __device__ __forceinline__ void finish(int nb) const {
+        bf16x8 o[2];
+        epi16_blk<PREC, RELU, MASK>(acc[nb], o, mw, nb);
+        dst->put(0, nb, InBlk<PREC>{{o[0], o[1]}});
+    }
+};
 
 // acc1[t][r] += A(row block nb0 + r) . in[t]   (r < N1)
 // acc2[t][r] += A(row block nb0 + N1 + r) . in[t]   (r < N2)
 // over KBN consecutive stream chunks (k blocks).
-template <int PREC, int TPW, int N1, int N2, int KBN, int G, int NT, class Src>
+template <int PREC, int TPW, int N1, int N2, int KBN, int G, int NT, class Src, class Epi = NoEpi>
 __device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1],
                                             f32x16 (&acc2)[TPW][N2 > 0 ? N2 : 1], int nb0, const Src& src,
                                             Ring& ring, Stager<G, NT>& st, const char* __restrict__ packed,
                                             const StreamDesc& sd, int tid, int lane,
-                                            const Sink<PREC, TPW>& sink = Sink<PREC, TPW>{nullptr, 0, 0, 0u}) {
+                                            const Sink<PREC, TPW>& sink = Sink<PREC, TPW>{nullptr, 0, 0, 0u},
+                                            const Epi& epi = Epi{}) {
+    static_assert(!Epi::kOn || (k16<PREC> && TPW == 1 && N2 == 0), "epilogue hook: 16-bit, one tile");
+    // Chunk sizes, read once per segment: every chunk of a segment has this
+    // segment's size; the prefetch in its last step is the next segment's first chunk.
+    const int q0 = ring.q;
+    const int ckb_this = sd.ckb[q0], adv_this = sd.cadv[q0];
+    const bool has_next = q0 + KBN < sd.nq;
+    const int ckb_next = has_next ? sd.ckb[q0 + KBN] : 0, adv_next = has_next ? sd.cadv[q0 + KBN] : 0;
 #pragma unroll
     for (int kb = 0; kb < KBN; ++kb) {
-        st.load(ring, sd, ring.q + 1, tid);
+        if (kb < KBN - 1)
+            st.load_sized(ring, ring.q + 1, ckb_this, adv_this, tid);
+        else if (has_next)
+            st.load_sized(ring, ring.q + 1, ckb_next, adv_next, tid);
         asm volatile("" ::: "memory");  // the sink stores below stay younger than the DMA
         const char* slot = ring.lds + (ring.q & 1) * ring.slot_bytes + lane16();
         InBlk<PREC> in[TPW];
+        constexpr bool B_ASM = k16<PREC> && Src::kLds;  // B operands read by asm (see A below)
+        if constexpr (B_ASM) {
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-            in[t] = src(t, kb);
-            sink(t, kb, in[t]);
+            for (int t = 0; t < TPW; ++t) ds_read_pair(in[t].s, src.addr(t, kb));
+        } else {
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) in[t] = src(t, kb);
         }
+        // 16-bit: the two A fragments of row block r + PF are read (inline asm) while
+        // row block r multiplies, and each MFMA pair waits (counted lgkmcnt, tied to its
+        // registers) only for its own reads.  Plain loads here get sunk by the compiler
+        // next to their use: one read, lgkmcnt(0), one MFMA, every time.
+        constexpr int NRB = N1 + N2;
+        constexpr int PF = NR_APF < NRB ? NR_APF : NRB;
+        bf16x8 aring[PF + 1][2];
+        const uint32_t abase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(slot)) +
+                               static_cast<uint32_t>(nb0 * kFPB<PREC> * kFragBytes);
+        if constexpr (k16<PREC>)
+#pragma unroll
+            for (int r = 0; r < PF; ++r) ds_read_pair(aring[r], abase + r * 2 * kFragBytes);
+        if constexpr (B_ASM)
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) lgkm_wait_pair(2 * PF + 2 * (TPW - 1 - t), in[t].s[0], in[t].s[1]);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) sink(t, kb, in[t]);
 #pragma unroll
         for (int r = 0; r < N1 + N2; ++r) {
             const char* fp = slot + (nb0 + r) * kFPB<PREC> * kFragBytes;
@@ -619,8 +736,11 @@ __device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1]
             const int r2 = r >= N1 ? (r - N1) % I2 : 0;
             (void)I1;
             if constexpr (k16<PREC>) {
-                const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(fp);
-                const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(fp + kFragBytes);
+                if (r + PF < NRB) ds_read_pair(aring[(r + PF) % (PF + 1)], abase + (r + PF) * 2 * kFragBytes);
+                bf16x8 a0 = aring[r % (PF + 1)][0];
+                bf16x8 a1 = aring[r % (PF + 1)][1];
+                const int younger = 2 * (NRB - 1 - r < PF ? NRB - 1 - r : PF);
+                lgkm_wait_pair(younger, a0, a1);
 #pragma unroll
                 for (int t = 0; t < TPW; ++t) {
                     if (r < N1) {
@@ -629,6 +749,12 @@ __device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1]
                     } else {
                         acc2[t][r2] = mfma16<PREC>(a0, in[t].s[0], acc2[t][r2]);
                         acc2[t][r2] = mfma16<PREC>(a1, in[t].s[1], acc2[t][r2]);
+                    }
+                }
+                if constexpr (Epi::kOn) {
+                    if (kb == KBN - 1) {
+                        if (r >= 1) epi.bias(r - 1);
+                        if (r >= 2) epi.finish(r - 2);
                     }
                 }
             } else {
@@ -645,6 +771,13 @@ __device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1]
                                 acc2[t][r2] = mfma_f32(a[e], in[t].v[4 * tq + e], acc2[t][r2]);
                         }
                 }
+            }
+        }
+        if constexpr (Epi::kOn) {
+            if (kb == KBN - 1) {
+                epi.bias(NRB - 1);
+                if (NRB >= 2) epi.finish(NRB - 2);
+                epi.finish(NRB - 1);
             }
         }
         st.store(ring.lds + ((ring.q + 1) & 1) * ring.slot_bytes, sd, ring.q + 1, tid, sink.stores());
@@ -734,6 +867,12 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) bl[nb] = lane < 32 ? a.params[a.bo[i] + 32 * nb + lane] : 0.f;
         const bool skip_in = i > 0 && ((a.skips >> (i - 1)) & 1u);
+        // 16-bit, one tile per wave: the epilogue runs inside the layer's last chunk
+        constexpr bool HOOK = k16<PREC> && TPW == 1 && NR_EPI_HOOK;
+        if constexpr (HOOK)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[q] = 0u;
+        const LayerEpi<PREC, true, TRAIN, decltype(hin)> ep{acc[0], bl, &hin, w};
         if (i == 0 || skip_in) {
             // x_enc is not kept in registers: the skip layer reloads the saved
             // copy (training) or recomputes it (inference)
@@ -768,14 +907,30 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                         if (tok[t]) store_img<PREC>(a.saved + a.sv_off[SV_XENC], tile0 + t, XB, kb, xe.v[t][kb], lane);
                 }
             }
-            stream_gemm<PREC, TPW, kHB, 0, XB, G, NT>(acc, dummy, 0, xe, ring, st, a.packed, a.sd, tid, lane);
+            bool hooked = false;
+            if constexpr (HOOK) {
+                if (i == 0) {
+                    stream_gemm<PREC, TPW, kHB, 0, XB, G, NT>(acc, dummy, 0, xe, ring, st, a.packed, a.sd, tid, lane,
+                                                              Sink<PREC, TPW>{nullptr, 0, 0, 0u}, ep);
+                    hooked = true;
+                }
+            }
+            if (!hooked)
+                stream_gemm<PREC, TPW, kHB, 0, XB, G, NT>(acc, dummy, 0, xe, ring, st, a.packed, a.sd, tid, lane);
         }
-        if (i > 0)
-            stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane,
-                                                       sink_of(SV_H0 + i - 1, kHB));
+        if (i > 0) {
+            if constexpr (HOOK)
+                stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane,
+                                                           sink_of(SV_H0 + i - 1, kHB), ep);
+            else
+                stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane,
+                                                           sink_of(SV_H0 + i - 1, kHB));
+        }
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-            if constexpr (k16<PREC>) {
+            if constexpr (HOOK) {
+                // done inside the stream
+            } else if constexpr (k16<PREC>) {
                 bf16x8 hv[kHB][2];
                 if (NR_BIASMFMA) {
 #pragma unroll
@@ -828,11 +983,23 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
-    stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane,
-                                               sink_of(SV_H0 + n - 1, kHB));
+    constexpr bool HOOKF = k16<PREC> && TPW == 1 && NR_EPI_HOOK;
+    if constexpr (HOOKF) {
+        float bf[kHB];
+#pragma unroll
+        for (int nb = 0; nb < kHB; ++nb) bf[nb] = lane < 32 ? a.params[a.bo[n] + 32 * nb + lane] : 0.f;
+        const LayerEpi<PREC, false, false, decltype(hin)> epf{acc[0], bf, &hin, w};
+        stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane,
+                                                   sink_of(SV_H0 + n - 1, kHB), epf);
+    } else {
+        stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane,
+                                                   sink_of(SV_H0 + n - 1, kHB));
+    }
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        if constexpr (k16<PREC>) {
+        if constexpr (HOOKF) {
+            // done inside the stream
+        } else if constexpr (k16<PREC>) {
             bf16x8 hv[kHB][2];
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) {
