@@ -1285,6 +1285,11 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
+    // the ReLU masks this stream's output needs are loaded before it (the stream's
+    // asm barriers keep loads from being hoisted over it by the compiler)
+    u32x4 mwf[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) mwf[t] = mask_of(t, n - 1);
     stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane,
                                                sink_of(a.ws_feat, kHB));
     {
@@ -1301,11 +1306,10 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        const u32x4 mwf = mask_of(t, n - 1);
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb) {
             InBlk<PREC> v;
-            to_in_masked<PREC>(acc[t][nb], mwf, nb, v);
+            to_in_masked<PREC>(acc[t][nb], mwf[t], nb, v);
             hin.put(t, nb, v);
             if ((n == 1 && !WANT_X) || !NR_SINK_BWD)  // (dz_0 without g_x has no consumer stream)
                 store_dz(WS_DZ0 + n - 1, kHB, t, nb, v);
@@ -1324,6 +1328,9 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
         for (int t = 0; t < TPW; ++t)
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
+        u32x4 mwt[TPW];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) mwt[t] = mask_of(t, i - 1);
         if ((a.skips >> (i - 1)) & 1u) {
             // W^T row blocks of a skip layer are [h (8) | x_enc (XB)]; without g_x
             // only the h rows are streamed
@@ -1339,11 +1346,10 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
         }
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-            const u32x4 mwt = mask_of(t, i - 1);
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) {
                 InBlk<PREC> v;
-                to_in_masked<PREC>(acc[t][nb], mwt, nb, v);
+                to_in_masked<PREC>(acc[t][nb], mwt[t], nb, v);
                 hin.put(t, nb, v);
                 if ((i == 1 && !WANT_X) || !NR_SINK_BWD)  // (dz_0 without g_x has no consumer stream)
                     store_dz(WS_DZ0 + i - 1, kHB, t, nb, v);
