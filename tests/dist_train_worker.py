@@ -1,0 +1,60 @@
+"""Worker of tests/test_distributed_gpu.py: the data-parallel Trainer step on the GPU.
+
+Every rank builds the same two networks (seed 42), takes its contiguous slice of one
+global batch (SURVEY.md §8e partitioning) and runs the engine.Trainer step whose
+per-network gradient all-reduce hooks into the MLP backward.  The ranks share one
+GPU here, so the collective is gloo over device tensors (RCCL refuses two ranks on
+one device); the hook/launch/finish path is the one bench.py runs over RCCL.
+Writes its final flat parameters to <out>/rank<r>.pt.
+"""
+
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "robust-nerf_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    out = Path(sys.argv[1])
+    steps = int(sys.argv[2])
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    pg = None
+    if world > 1:
+        dist.init_process_group("gloo")
+        pg = dist.group.WORLD
+    from noisy_src.config import ModelConfig, RenderConfig
+    from noisy_src.engine import Trainer
+    from noisy_src.model import create_nerf
+    from bench import lego_rays
+
+    torch.manual_seed(42)
+    mc, mf = create_nerf(ModelConfig(precision="fp32"))
+    mc, mf = mc.to(dev), mf.to(dev)
+    rc = RenderConfig()
+    trainer = Trainer(mc, mf, rc, process_group=pg)
+    B = 256
+    per = B // world
+    for k in range(steps):
+        o, d, t = lego_rays(B, 500 + k, dev)
+        g = torch.Generator().manual_seed(900 + k)
+        tr = torch.rand(B, rc.num_samples, generator=g).to(dev)
+        u = torch.rand(B, rc.num_samples_fine, generator=g).to(dev)
+        sl = slice(rank * per, (rank + 1) * per)
+        trainer.step(o[sl], d[sl], t[sl], t_rand=tr[sl], u=u[sl])
+    torch.cuda.synchronize()
+    flat = torch.cat([mc.flat_params().cpu(), mf.flat_params().cpu()])
+    torch.save(flat, out / f"rank{rank}_of{world}.pt")
+    if pg is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
