@@ -181,6 +181,12 @@ __device__ __forceinline__ void pe_feat_bwd(float x0, float x1, float x2, int f,
 #ifndef NR_APF
 #define NR_APF 3  // 16-bit weight-stream A fragments read ahead (row blocks)
 #endif
+#ifndef NR_AB_NOWAIT
+#define NR_AB_NOWAIT 0
+#endif
+#ifndef NR_AB_HALFA
+#define NR_AB_HALFA 0
+#endif
 #ifndef NR_AB_NODMA
 #define NR_AB_NODMA 0  // A/B timing only (wrong results): no weight-stream DMA
 #endif
@@ -517,6 +523,7 @@ struct Stager {
     // ops issued since (the chunk's saved-activation / dz stores) may stay in flight
     // across the barrier (vmcnt retires in issue order).
     __device__ __forceinline__ void store(char*, const StreamDesc&, int, int, int after = 0) {
+        if (NR_AB_NOWAIT) return;  // A/B timing only (racy)
         switch (after) {
             case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
             case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
@@ -621,7 +628,11 @@ __device__ __forceinline__ void stream_barrier() {
 // see stream_gemm) and the counted wait that publishes them.
 __device__ __forceinline__ void ds_read_pair(bf16x8 (&dst)[2], uint32_t addr) {
     asm volatile("ds_read_b128 %0, %1" : "=v"(dst[0]) : "v"(addr));
+#if NR_AB_HALFA  // A/B timing only (wrong results): half the LDS read traffic
+    dst[1] = dst[0];
+#else
     asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(dst[1]) : "v"(addr));
+#endif
 }
 // wait until at most n LDS/SMEM ops are outstanding (n: the reads issued after
 // these two, all younger LDS reads; SMEM only ever makes this wait longer)

@@ -132,4 +132,57 @@ def train(config: NeRFConfig, train_data: BlenderData, val_data: Optional[Blende
     return result
 
 
-__all__ = ["set_seed", "train_step", "render_image", "evaluate", "train", "lr_lambda_factory"]
+def main(argv=None) -> None:
+    """``python -m noisy_src.train`` — the reference CLI (train.py:580-640), same flags
+    plus ``--precision``; needs the NeRF synthetic scene under ``--data_root``."""
+    import argparse
+    from pathlib import Path
+
+    from .config import DataConfig, ModelConfig, RenderConfig, TrainConfig
+    from .data import load_blender_data
+    from .logger import ExperimentLogger, ValidationMetrics
+
+    ap = argparse.ArgumentParser(description="NeRF training (MI355X HIP path)")
+    ap.add_argument("--scene", type=str, default="lego")
+    ap.add_argument("--data_root", type=str, default=None)
+    ap.add_argument("--img_scale", type=float, default=0.5)
+    ap.add_argument("--batch_size", type=int, default=1024)
+    ap.add_argument("--num_iters", type=int, default=200000)
+    ap.add_argument("--lr", type=float, default=5e-4)
+    ap.add_argument("--no_hierarchical", action="store_true")
+    ap.add_argument("--num_samples", type=int, default=64)
+    ap.add_argument("--num_samples_fine", type=int, default=128)
+    ap.add_argument("--log_every", type=int, default=100)
+    ap.add_argument("--val_every", type=int, default=5000)
+    ap.add_argument("--output_dir", type=str, default="outputs")
+    ap.add_argument("--exp_name", type=str, default="auto")
+    ap.add_argument("--device", type=str, default="cuda")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16", "fp16"])
+    a = ap.parse_args(argv)
+    cfg = NeRFConfig(
+        model=ModelConfig(precision=a.precision),
+        render=RenderConfig(num_samples=a.num_samples, num_samples_fine=a.num_samples_fine,
+                            use_hierarchical=not a.no_hierarchical),
+        data=DataConfig(scene_name=a.scene, data_root=Path(a.data_root) if a.data_root else None,
+                        img_scale=a.img_scale, batch_size=a.batch_size),
+        train=TrainConfig(lr=a.lr, num_iterations=a.num_iters, log_every=a.log_every, val_every=a.val_every,
+                          output_dir=Path(a.output_dir), experiment_name=a.exp_name, device=a.device, seed=a.seed))
+    root = cfg.data.data_root or Path("data") / "raw"
+    train_data = load_blender_data(root, a.scene, "train", a.img_scale, a.device)
+    val_data = load_blender_data(root, a.scene, "val", a.img_scale, a.device)
+    name = a.exp_name if a.exp_name != "auto" else f"{a.scene}_clean_{time.strftime('%Y%m%d_%H%M%S')}"
+    logger = ExperimentLogger(Path(a.output_dir) / name, name)
+    logger.log_config(cfg)
+    res = train(cfg, train_data, val_data)
+    if "val" in res:
+        v = res["val"]
+        logger.log_validation(ValidationMetrics(iteration=a.num_iters, psnr=v["psnr"], ssim=v["ssim"], mse=v["mse"],
+                                                per_image_psnr=v["per_image_psnr"], per_image_ssim=v["per_image_ssim"]))
+    logger.close()
+
+
+__all__ = ["set_seed", "train_step", "render_image", "evaluate", "train", "lr_lambda_factory", "main"]
+
+if __name__ == "__main__":
+    main()

@@ -203,3 +203,131 @@ def evaluate_with_poses(model_coarse: NeRF, model_fine: Optional[NeRF], camera_p
         ssim.append(compute_ssim(pred, target).item())
     return {"iteration": iteration, "psnr": float(np.mean(psnr)), "ssim": float(np.mean(ssim)),
             "mse": float(np.mean(mse)), "lpips": None, "per_image_psnr": psnr, "per_image_ssim": ssim}
+
+
+def train_with_pose_optimization(config, train_data: BlenderData, val_data: Optional[BlenderData] = None,
+                                 init_mode: str = "noisy", noise_config=None, pose_lr: float = 1e-4,
+                                 pose_opt_delay: int = 1000, learn_rotation: bool = True,
+                                 learn_translation: bool = True, rotation_reg_weight: float = 0.01,
+                                 translation_reg_weight: float = 0.001, logger=None, log=print) -> Dict[str, object]:
+    """Reference train_pose_opt.py:613-1054 without the image/checkpoint I/O: seeds, noisy
+    (or clean) initial poses, CameraPoseParameters, both networks, NeRF and pose Adams
+    (fused) with their LambdaLRs (the pose one steps only once poses optimise), the
+    pixel sampler, and train_step_with_poses every iteration."""
+    import time
+
+    from .data_pose_opt import create_pixel_dataset
+    from .engine import lr_lambda_factory
+    from .logger import TrainingMetrics
+    from .model import create_nerf
+    from .noise import add_noise_to_poses
+
+    set_seed(config.train.seed)
+    dev = train_data.images.device
+    gt = train_data.poses.clone()
+    if init_mode == "noisy" and noise_config is not None and noise_config.has_noise:
+        init, _ = add_noise_to_poses(train_data.poses, noise_config)
+    else:
+        init = gt.clone()
+    cam = CameraPoseParameters(init, learn_rotation, learn_translation).to(dev)
+    mc, mf = create_nerf(config.model)
+    mc = mc.to(dev)
+    mf = mf.to(dev) if config.render.use_hierarchical else None
+    nerf_params = list(mc.parameters()) + (list(mf.parameters()) if mf is not None else [])
+    opt_n = FusedAdam(nerf_params, lr=config.train.lr)
+    opt_p = FusedAdam(cam.parameters(), lr=pose_lr)
+    lam = lr_lambda_factory(config.train.lr_decay)
+    sch_n = torch.optim.lr_scheduler.LambdaLR(opt_n, lam)
+    sch_p = torch.optim.lr_scheduler.LambdaLR(opt_p, lam)
+    _, sampler = create_pixel_dataset(train_data)
+    sampler.batch_size = config.data.batch_size
+    t0 = time.time()
+    for it in range(config.train.num_iterations):
+        batch = sampler.sample_batch()
+        now = it >= pose_opt_delay
+        tb = time.time()
+        m = train_step_with_poses(mc, mf, cam, sampler, opt_n, opt_p if now else None, batch, config.render,
+                                  optimize_poses=now, rotation_reg_weight=rotation_reg_weight,
+                                  translation_reg_weight=translation_reg_weight)
+        sch_n.step()
+        if now:
+            sch_p.step()
+        dt = time.time() - tb
+        if logger is not None:
+            logger.log_training(TrainingMetrics(iteration=it, loss=m["loss"], loss_coarse=m["loss_coarse"],
+                                                loss_fine=m.get("loss_fine"), psnr=m["psnr"],
+                                                learning_rate=opt_n.param_groups[0]["lr"], time_per_iter=dt,
+                                                rays_per_sec=config.data.batch_size / dt))
+        if it % config.train.log_every == 0:
+            log(f"iter {it}: loss {m['loss']:.5f} psnr {m['psnr']:.2f} poses {'on' if now else 'frozen'} "
+                f"({time.time() - t0:.1f} s)")
+    out = {"model_coarse": mc, "model_fine": mf, "camera_params": cam,
+           "pose_errors": cam.compute_pose_errors(gt)}
+    if val_data is not None:
+        out["val"] = evaluate_with_poses(mc, mf, cam, val_data, torch.arange(val_data.images.shape[0]), config.render)
+    return out
+
+
+def main(argv=None) -> None:
+    """``python -m noisy_src.train_pose_opt`` — the reference CLI (train_pose_opt.py:1057-1190),
+    same flags plus ``--precision``; needs the NeRF synthetic scene under ``--data_root``."""
+    import argparse
+    from pathlib import Path
+
+    from .config import DataConfig, ModelConfig, NeRFConfig, TrainConfig
+    from .data import load_blender_data
+    from .logger import ExperimentLogger
+    from .noise import NoiseConfig
+
+    ap = argparse.ArgumentParser(description="Joint NeRF + camera pose optimisation (MI355X HIP path)")
+    ap.add_argument("--scene", type=str, default="lego")
+    ap.add_argument("--data_root", type=str, default=None)
+    ap.add_argument("--img_scale", type=float, default=0.5)
+    ap.add_argument("--batch_size", type=int, default=1024)
+    ap.add_argument("--num_iters", type=int, default=50000)
+    ap.add_argument("--lr", type=float, default=5e-4)
+    ap.add_argument("--init_mode", type=str, default="noisy", choices=["noisy", "clean"])
+    ap.add_argument("--pose_lr", type=float, default=1e-4)
+    ap.add_argument("--pose_opt_delay", type=int, default=1000)
+    ap.add_argument("--no_learn_rotation", action="store_true")
+    ap.add_argument("--no_learn_translation", action="store_true")
+    ap.add_argument("--rotation_reg_weight", type=float, default=0.01)
+    ap.add_argument("--translation_reg_weight", type=float, default=0.001)
+    ap.add_argument("--rotation_noise", type=float, default=0.0)
+    ap.add_argument("--translation_noise", type=float, default=0.0)
+    ap.add_argument("--translation_noise_pct", type=float, default=0.0)
+    ap.add_argument("--noise_seed", type=int, default=None)
+    ap.add_argument("--no_hierarchical", action="store_true")
+    ap.add_argument("--num_samples", type=int, default=64)
+    ap.add_argument("--num_samples_fine", type=int, default=128)
+    ap.add_argument("--log_every", type=int, default=100)
+    ap.add_argument("--output_dir", type=str, default="outputs")
+    ap.add_argument("--device", type=str, default="cuda")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16", "fp16"])
+    a = ap.parse_args(argv)
+    cfg = NeRFConfig(
+        model=ModelConfig(precision=a.precision),
+        render=RenderConfig(num_samples=a.num_samples, num_samples_fine=a.num_samples_fine,
+                            use_hierarchical=not a.no_hierarchical),
+        data=DataConfig(scene_name=a.scene, data_root=Path(a.data_root) if a.data_root else None,
+                        img_scale=a.img_scale, batch_size=a.batch_size),
+        train=TrainConfig(lr=a.lr, num_iterations=a.num_iters, log_every=a.log_every,
+                          output_dir=Path(a.output_dir), device=a.device, seed=a.seed))
+    noise = NoiseConfig(rotation_noise_deg=a.rotation_noise, translation_noise=a.translation_noise,
+                        translation_noise_pct=a.translation_noise_pct, seed=a.noise_seed)
+    root = cfg.data.data_root or Path("data") / "raw"
+    train_data = load_blender_data(root, a.scene, "train", a.img_scale, a.device)
+    val_data = load_blender_data(root, a.scene, "val", a.img_scale, a.device)
+    import time
+    name = f"{a.scene}_poseopt_{a.init_mode}init_{noise}_{time.strftime('%Y%m%d_%H%M%S')}"  # (:274-287)
+    logger = ExperimentLogger(Path(a.output_dir) / name, name)
+    logger.log_config(cfg)
+    train_with_pose_optimization(cfg, train_data, val_data, a.init_mode, noise, a.pose_lr, a.pose_opt_delay,
+                                 not a.no_learn_rotation, not a.no_learn_translation, a.rotation_reg_weight,
+                                 a.translation_reg_weight, logger=logger)
+    logger.close()
+
+
+if __name__ == "__main__":
+    main()
