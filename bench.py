@@ -99,6 +99,22 @@ def lego_rays(n_rays: int, seed: int, device):
     return o.to(device), d.to(device), tgt.to(device)
 
 
+def pose_opt_setup(H: int, W: int, device):
+    """BASELINE cfg #3 inputs: the lego training cameras (GT poses of the reference's
+    final_poses.pt fixture), the reference's own noisy initialisation for 5 deg rotation +
+    5 % translation noise (initial_poses of that run's fixture) as the learnable poses,
+    and an H x W synthetic image stack for the pixel sampler (train_pose_opt.py:640-700)."""
+    from noisy_src.data import synthetic_blender_data
+    from noisy_src.data_pose_opt import create_pixel_dataset
+    from noisy_src.train_pose_opt import CameraPoseParameters
+    fix = sorted((ROOT / "tests" / "golden").glob("final_poses_*rot5.0deg_trans5.0pct_*.npz"))[0]
+    z = np.load(fix)
+    data = synthetic_blender_data(torch.from_numpy(z["ground_truth_poses"]), H=H, W=W, device=device)
+    cam = CameraPoseParameters(torch.from_numpy(z["initial_poses"]).to(device))
+    _, sampler = create_pixel_dataset(data)
+    return cam, sampler
+
+
 def psnr_record():
     """Summary of profiles/r01_psnr_parity.json (tests/psnr_parity.py, run on the GPU box):
     test PSNR at equal iterations of this engine vs the oracle, not measured in this run."""
@@ -149,6 +165,8 @@ def main():
     ap.add_argument("--cpu-rays", type=int, default=1024)
     ap.add_argument("--cpu-steps", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pose-opt", action="store_true",
+                    help="BASELINE cfg #3: joint pose optimisation step (train_pose_opt, poses optimising)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -164,20 +182,30 @@ def main():
 
     from noisy_src import _hip
     from noisy_src.config import ModelConfig, RenderConfig
-    from noisy_src.engine import Trainer
+    from noisy_src.engine import PoseTrainer, Trainer
     from noisy_src.model import create_nerf
 
     torch.manual_seed(42)  # train.py:319 set_seed(42); identical init on every rank
     mc, mf = create_nerf(ModelConfig(precision=args.precision))
     mc, mf = mc.to(dev), mf.to(dev)
     rcfg = RenderConfig(num_samples=args.num_samples, num_samples_fine=args.num_samples_fine)
-    trainer = Trainer(mc, mf, rcfg, process_group=pg)
-
     B = args.batch
-    pool = [lego_rays(B, 1000 * rank + k, dev) for k in range(4)]
+    if args.pose_opt:
+        # rays come from (image, pixel) and the learnable poses INSIDE the step; the
+        # pixel draws (sampler.sample_batch) stay outside it, as batch sampling does below
+        cam, sampler = pose_opt_setup(800, 800, dev)
+        sampler.batch_size = B
+        trainer = PoseTrainer(mc, mf, cam, sampler, rcfg, process_group=pg)
+        gen = torch.Generator(device=dev).manual_seed(1000 * rank)
+        pool = [sampler.sample_batch(generator=gen) for _ in range(4)]
+    else:
+        trainer = Trainer(mc, mf, rcfg, process_group=pg)
+        pool = [lego_rays(B, 1000 * rank + k, dev) for k in range(4)]
     torch.manual_seed(1234 + rank)
 
     def step(k):
+        if args.pose_opt:
+            return trainer.step(pool[k % len(pool)], optimize_poses=True)
         o, d, t = pool[k % len(pool)]
         return trainer.step(o, d, t)
 
@@ -232,8 +260,9 @@ def main():
         "dtype": args.precision,
         "data": "synthetic (lego 800x800 camera rays from the reference's GT poses; random targets)",
         "config": {
-            "workload": f"lego 800x800 hierarchical {rcfg.num_samples}c+{rcfg.num_samples_fine}f training step, "
-                        f"{B} rays per GPU",
+            "workload": (f"lego 800x800 joint pose-opt (5 deg rot + 5% trans noisy init, SE(3) pose grads) "
+                         if args.pose_opt else "lego 800x800 ")
+                        + f"hierarchical {rcfg.num_samples}c+{rcfg.num_samples_fine}f training step, {B} rays per GPU",
             "global_batch": world * B,
             "num_samples": rcfg.num_samples,
             "num_samples_fine": rcfg.num_samples_fine,
@@ -261,7 +290,7 @@ def main():
         # metric is the recorded equal-iteration comparison on the analytic scene
         "psnr": psnr_record(),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.pose_opt:
         out["cpu_baseline"] = cpu_baseline(args.cpu_rays, args.cpu_steps)
     if rank == 0:
         print(json.dumps(out))

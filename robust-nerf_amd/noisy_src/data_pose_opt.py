@@ -29,6 +29,10 @@ class PixelBatch:
     pixel_coords: torch.Tensor   # (B, 2) float (u, v)
     target_rgb: torch.Tensor     # (B, 3)
 
+    def slice(self, sl: slice) -> "PixelBatch":
+        """Rows ``sl`` of the batch (a data-parallel rank's contiguous share)."""
+        return PixelBatch(self.image_indices[sl], self.pixel_coords[sl], self.target_rgb[sl])
+
 
 class PixelDataset:
     """Reference data_pose_opt.py:29-148."""
@@ -65,8 +69,10 @@ class PixelSampler:
         self.device = dataset.device
         self.n_pixels = dataset.n_pixels
 
-    def sample_batch(self) -> PixelBatch:
-        idx = torch.randint(0, self.n_pixels, (self.batch_size,), device=self.device)
+    def sample_batch(self, generator=None) -> PixelBatch:
+        """``generator`` (optional, on the dataset's device) makes the draw reproducible
+        across data-parallel ranks that each take a slice of it."""
+        idx = torch.randint(0, self.n_pixels, (self.batch_size,), device=self.device, generator=generator)
         ds = self.dataset
         return PixelBatch(image_indices=ds.image_indices[idx], pixel_coords=ds.pixel_coords[idx],
                           target_rgb=ds.target_rgb[idx])

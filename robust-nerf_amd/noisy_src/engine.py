@@ -102,6 +102,91 @@ class Trainer:
         return metrics
 
 
+class PoseTrainer:
+    """The joint pose-optimisation step without host synchronisation (BASELINE cfg #3).
+
+    Mirrors ``train_step_with_poses`` of the reference (noisy_src/train_pose_opt.py:290-411)
+    plus the two ``scheduler.step()`` of its loop (:876-880): all poses from the SE(3)
+    kernel, the batch's rays from (image, pixel) and those poses, render coarse+fine, MSE
+    losses plus the pose regulariser (0.01 mean w^2 + 0.001 mean dt^2, :377-389, weights
+    :621-622), backward, separate clips (coarse 1.0, fine 1.0, poses 0.1, :398-404) fused
+    into the Adams, the pose Adam and its LambdaLR only once ``optimize_poses``.  The
+    reference's ``.item()`` metrics are left to the caller (losses stay on the device).
+    Data parallel: the network gradients all-reduce as in ``Trainer``; the pose gradient
+    (each rank touches its own images) is one more all-reduce of 2 x 3 x n_poses floats,
+    whose SUM over ranks is the single-process gradient."""
+
+    def __init__(self, model_coarse, model_fine, camera_params, pixel_sampler, render_config,
+                 lr: float = 5e-4, pose_lr: float = 1e-4, lr_decay: int = 250,
+                 rotation_reg_weight: float = 0.01, translation_reg_weight: float = 0.001, process_group=None):
+        self.model_coarse, self.model_fine = model_coarse, model_fine
+        self.camera_params, self.pixel_sampler, self.render_config = camera_params, pixel_sampler, render_config
+        self.coarse = list(model_coarse.parameters())
+        self.fine = list(model_fine.parameters()) if model_fine is not None else []
+        self.poses = list(camera_params.parameters())
+        self.rot_w, self.trans_w = rotation_reg_weight, translation_reg_weight
+        self.optimizer_nerf = FusedAdam(self.coarse + self.fine, lr=lr)
+        self.optimizer_poses = FusedAdam(self.poses, lr=pose_lr) if self.poses else None
+        lam = lr_lambda_factory(lr_decay)
+        self.scheduler_nerf = torch.optim.lr_scheduler.LambdaLR(self.optimizer_nerf, lam)
+        self.scheduler_poses = (torch.optim.lr_scheduler.LambdaLR(self.optimizer_poses, lam)
+                                if self.optimizer_poses is not None else None)
+        self.reducer = None
+        if process_group is not None:
+            self.reducer = GradAllReducer(process_group)
+            for net in (model_coarse, model_fine):
+                if net is not None:
+                    net._grad_ready_hook = self.reducer.launch
+
+    def step(self, pixel_batch, optimize_poses: bool = True, t_rand: Optional[torch.Tensor] = None,
+             u: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+        cam = self.camera_params
+        optimize_poses = optimize_poses and self.optimizer_poses is not None
+        self.optimizer_nerf.zero_grad(set_to_none=True)
+        if optimize_poses:
+            self.optimizer_poses.zero_grad(set_to_none=True)
+        rays_o, rays_d = self.pixel_sampler.get_rays_for_batch(pixel_batch, cam.get_all_poses())
+        target = pixel_batch.target_rgb
+        out = render_rays(self.model_coarse, self.model_fine, rays_o, rays_d, self.render_config, is_train=True,
+                          t_rand=t_rand, u=u)
+        loss_c = ops.mse_loss(out["rgb_coarse"], target)
+        loss = loss_c
+        metrics = {"loss_coarse": loss_c}
+        if "rgb_fine" in out:
+            loss_f = ops.mse_loss(out["rgb_fine"], target)
+            loss = loss_c + loss_f
+            metrics["loss_fine"] = loss_f
+        if optimize_poses:
+            if self.rot_w > 0 and cam.learn_rotation:
+                loss = loss + self.rot_w * torch.mean(cam.rotation_deltas ** 2)
+            if self.trans_w > 0 and cam.learn_translation:
+                loss = loss + self.trans_w * torch.mean(cam.translation_deltas ** 2)
+        loss.backward()
+        if self.reducer is not None:
+            flats = [flat for _, flat in self.reducer.pending]
+            pg = [p.grad for p in self.poses if p.grad is not None] if optimize_poses else []
+            pflat = torch.cat([g.reshape(-1) for g in pg]) if pg else None
+            if pflat is not None:
+                self.reducer.launch(pflat)
+            self.reducer.finish()
+            for net in (self.model_coarse, self.model_fine):
+                if net is not None:
+                    _adopt_reduced_grad(net, flats)
+            off = 0
+            for g in pg:
+                g.copy_(pflat[off:off + g.numel()].view(g.shape))
+                off += g.numel()
+        groups = [(self.coarse, 1.0)] + ([(self.fine, 1.0)] if self.fine else [])
+        self.optimizer_nerf.step(clip_groups=groups)
+        self.scheduler_nerf.step()
+        if optimize_poses:
+            self.optimizer_poses.step(clip_groups=[(self.poses, 0.1)])
+            self.scheduler_poses.step()
+        metrics["loss"] = loss.detach()
+        metrics["rgb_fine"] = out.get("rgb_fine", out["rgb_coarse"]).detach()
+        return metrics
+
+
 def _adopt_reduced_grad(net, flats) -> None:
     """The MLP backward hands autograd views of its flat gradient, which AccumulateGrad
     normally adopts as ``.grad``; if it copied them instead, copy the reduced values."""

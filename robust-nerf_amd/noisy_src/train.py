@@ -6,8 +6,8 @@ NeRF training step and image rendering — drop-in for ShawnnnLiu/Robust-NeRF
 returned metrics (train.py:68-119: four host syncs for the logged scalars, joint
 clip at 1.0 over both networks).  With the package's ``FusedAdam`` the clip folds
 into the fused update.  ``engine.Trainer`` is the same step without the host syncs,
-which is what ``bench.py`` times.  ``train`` is a minimal loop over a ``RaySampler``
-(logging/checkpoint I/O are out of scope).
+which is what ``bench.py`` times.  ``train`` is a minimal loop over a ``RaySampler``;
+``save_checkpoint`` / ``load_checkpoint`` keep the reference's checkpoint format.
 """
 
 from __future__ import annotations
@@ -99,6 +99,49 @@ def evaluate(renderer: NeRFRenderer, val_data: BlenderData, num_images: int = 5,
             "per_image_psnr": psnr, "per_image_ssim": ssim}
 
 
+def save_checkpoint(output_dir, iteration: int, model_coarse, model_fine, optimizer: torch.optim.Optimizer,
+                    config: NeRFConfig, noise_config=None, metrics: Optional[Dict] = None,
+                    is_best: bool = False) -> None:
+    """Reference train.py:236-286: same keys (iteration, model_coarse/_fine state_dicts in
+    nn.Linear naming, optimizer state, config as plain dicts), same file names.  The config
+    values are made plain (Path -> str, tuple -> list) so that ``torch.load(...,
+    weights_only=True)`` reads the file back."""
+    from pathlib import Path
+
+    def plain(d):
+        return {k: str(v) if isinstance(v, Path) else list(v) if isinstance(v, tuple) else v for k, v in d.items()}
+
+    output_dir = Path(output_dir)
+    output_dir.mkdir(parents=True, exist_ok=True)
+    ckpt = {"iteration": iteration, "model_coarse": model_coarse.state_dict(), "optimizer": optimizer.state_dict(),
+            "config": {"model": plain(config.model.__dict__), "render": plain(config.render.__dict__),
+                       "data": plain(config.data.__dict__), "train": plain(config.train.__dict__)}}
+    if model_fine is not None:
+        ckpt["model_fine"] = model_fine.state_dict()
+    if metrics is not None:
+        ckpt["metrics"] = metrics
+    if noise_config is not None:
+        ckpt["noise_config"] = {"rotation_noise_deg": noise_config.rotation_noise_deg,
+                                "translation_noise": noise_config.translation_noise,
+                                "translation_noise_pct": noise_config.translation_noise_pct,
+                                "seed": noise_config.seed}
+    torch.save(ckpt, output_dir / f"checkpoint_{iteration:07d}.pt")
+    torch.save(ckpt, output_dir / "checkpoint_latest.pt")
+    if is_best:
+        torch.save(ckpt, output_dir / "checkpoint_best.pt")
+
+
+def load_checkpoint(checkpoint_path, model_coarse, model_fine, optimizer: Optional[torch.optim.Optimizer] = None) -> int:
+    """Reference train.py:289-304 -> iteration (``weights_only=True``)."""
+    ckpt = torch.load(checkpoint_path, map_location=next(model_coarse.parameters()).device, weights_only=True)
+    model_coarse.load_state_dict(ckpt["model_coarse"])
+    if model_fine is not None and "model_fine" in ckpt:
+        model_fine.load_state_dict(ckpt["model_fine"])
+    if optimizer is not None and "optimizer" in ckpt:
+        optimizer.load_state_dict(ckpt["optimizer"])
+    return ckpt.get("iteration", 0)
+
+
 def train(config: NeRFConfig, train_data: BlenderData, val_data: Optional[BlenderData] = None,
           num_iterations: Optional[int] = None, log=print) -> Dict[str, object]:
     """Reference train.py:307-577, minus logging/checkpoint I/O: seeds, builds the two
@@ -182,7 +225,8 @@ def main(argv=None) -> None:
     logger.close()
 
 
-__all__ = ["set_seed", "train_step", "render_image", "evaluate", "train", "lr_lambda_factory", "main"]
+__all__ = ["set_seed", "train_step", "render_image", "evaluate", "save_checkpoint", "load_checkpoint", "train",
+           "lr_lambda_factory", "main"]
 
 if __name__ == "__main__":
     main()

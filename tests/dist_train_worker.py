@@ -31,27 +31,39 @@ def main():
         dist.init_process_group("gloo")
         pg = dist.group.WORLD
     from noisy_src.config import ModelConfig, RenderConfig
-    from noisy_src.engine import Trainer
+    from noisy_src.engine import PoseTrainer, Trainer
     from noisy_src.model import create_nerf
-    from bench import lego_rays
+    from bench import lego_rays, pose_opt_setup
 
+    pose_mode = len(sys.argv) > 3 and sys.argv[3] == "pose"
     torch.manual_seed(42)
     mc, mf = create_nerf(ModelConfig(precision="fp32"))
     mc, mf = mc.to(dev), mf.to(dev)
     rc = RenderConfig()
-    trainer = Trainer(mc, mf, rc, process_group=pg)
     B = 256
     per = B // world
+    sl = slice(rank * per, (rank + 1) * per)
+    if pose_mode:
+        # joint pose optimisation (cfg #3): the pose gradient is one more all-reduce
+        cam, sampler = pose_opt_setup(64, 64, dev)
+        trainer = PoseTrainer(mc, mf, cam, sampler, rc, process_group=pg)
+    else:
+        trainer = Trainer(mc, mf, rc, process_group=pg)
     for k in range(steps):
-        o, d, t = lego_rays(B, 500 + k, dev)
         g = torch.Generator().manual_seed(900 + k)
         tr = torch.rand(B, rc.num_samples, generator=g).to(dev)
         u = torch.rand(B, rc.num_samples_fine, generator=g).to(dev)
-        sl = slice(rank * per, (rank + 1) * per)
-        trainer.step(o[sl], d[sl], t[sl], t_rand=tr[sl], u=u[sl])
+        if pose_mode:
+            batch = sampler.sample_batch(generator=torch.Generator(device=dev).manual_seed(700 + k))
+            trainer.step(batch.slice(sl), optimize_poses=True, t_rand=tr[sl], u=u[sl])
+        else:
+            o, d, t = lego_rays(B, 500 + k, dev)
+            trainer.step(o[sl], d[sl], t[sl], t_rand=tr[sl], u=u[sl])
     torch.cuda.synchronize()
     flat = torch.cat([mc.flat_params().cpu(), mf.flat_params().cpu()])
-    torch.save(flat, out / f"rank{rank}_of{world}.pt")
+    if pose_mode:
+        flat = torch.cat([flat, torch.cat([p.detach().reshape(-1).cpu() for p in cam.parameters()])])
+    torch.save(flat, out / f"{'pose_' if pose_mode else ''}rank{rank}_of{world}.pt")
     if pg is not None:
         dist.destroy_process_group()
 

@@ -39,3 +39,24 @@ def test_two_ranks_match_one_process(tmp_path):
     # ~0 can flip sign under a different summation order (see test_train_steps_match_oracle)
     assert diff.max() < 2 * steps * 5e-4
     assert (diff < 1e-5).float().mean() > 0.98
+
+
+def test_two_ranks_match_one_process_pose_opt(tmp_path):
+    """Joint pose optimisation (cfg #3) data parallel: the network all-reduces plus the
+    pose-gradient all-reduce give every rank the one-process update."""
+    steps = 2
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    subprocess.run([sys.executable, str(WORKER), str(tmp_path), str(steps), "pose"], check=True, env=env,
+                   timeout=300)
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                    "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(WORKER), str(tmp_path),
+                    str(steps), "pose"], check=True, env=env, timeout=300)
+    one = torch.load(tmp_path / "pose_rank0_of1.pt", weights_only=True)
+    r0 = torch.load(tmp_path / "pose_rank0_of2.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "pose_rank1_of2.pt", weights_only=True)
+    assert torch.equal(r0, r1)
+    n_pose = 2 * 3 * 100
+    assert (r0[:-n_pose] - one[:-n_pose]).abs().max() < 2 * steps * 5e-4
+    # poses: lr 1e-4, Adam moves each coordinate by <= ~lr per step
+    assert (r0[-n_pose:] - one[-n_pose:]).abs().max() < 2 * steps * 1e-4
+    assert one[-n_pose:].abs().max() > 0  # the translations moved

@@ -189,3 +189,46 @@ def test_render_image_matches_render_rays():
     val = synthetic_blender_data(_gt_poses()[:2], H=12, W=10, device=DEV)
     m = evaluate(NeRFRenderer(mc, mf, rc), val, num_images=2)
     assert np.isfinite(m["psnr"]) and 0 < m["ssim"] <= 1
+
+
+def test_pose_trainer_matches_train_step_with_poses():
+    """engine.PoseTrainer (the sync-free cfg #3 step bench.py --pose-opt times) performs
+    the same update as train_pose_opt.train_step_with_poses + its schedulers."""
+    from noisy_src.config import RenderConfig
+    from noisy_src.data import synthetic_blender_data
+    from noisy_src.data_pose_opt import PixelDataset, PixelSampler
+    from noisy_src.engine import PoseTrainer, lr_lambda_factory
+    from noisy_src.optim import FusedAdam
+    from noisy_src.train_pose_opt import CameraPoseParameters, train_step_with_poses
+    rc = RenderConfig()
+    init = _gt_poses()[:4].clone()
+    init[:, :3, 3] += 0.05
+    data = synthetic_blender_data(init, H=24, W=24, device=DEV)
+    sampler = PixelSampler(PixelDataset(data), batch_size=256)
+    _, _, mc_a, mf_a = _nets()
+    _, _, mc_b, mf_b = _nets()
+    cam_a, cam_b = CameraPoseParameters(init.to(DEV)), CameraPoseParameters(init.to(DEV))
+    opt_n = FusedAdam(list(mc_a.parameters()) + list(mf_a.parameters()), lr=5e-4)
+    opt_p = FusedAdam(cam_a.parameters(), lr=1e-4)
+    sch_n = torch.optim.lr_scheduler.LambdaLR(opt_n, lr_lambda_factory(250))
+    sch_p = torch.optim.lr_scheduler.LambdaLR(opt_p, lr_lambda_factory(250))
+    trainer = PoseTrainer(mc_b, mf_b, cam_b, sampler, rc)
+    for step in range(3):
+        now = step >= 1  # the first step stands for the pose-opt delay
+        batch = sampler.sample_batch(generator=torch.Generator(device=DEV).manual_seed(40 + step))
+        g = torch.Generator().manual_seed(50 + step)
+        tr, u = torch.rand(256, 64, generator=g).to(DEV), torch.rand(256, 128, generator=g).to(DEV)
+        got = train_step_with_poses(mc_a, mf_a, cam_a, sampler, opt_n, opt_p if now else None, batch, rc,
+                                    optimize_poses=now, rotation_reg_weight=0.01 if now else 0.0,
+                                    translation_reg_weight=0.001 if now else 0.0, t_rand=tr, u=u)
+        sch_n.step()
+        if now:
+            sch_p.step()
+        m = trainer.step(batch, optimize_poses=now, t_rand=tr, u=u)
+        assert abs(float(m["loss"]) - got["loss"]) < 1e-6, step
+    assert torch.equal(mc_a.flat_params(), mc_b.flat_params())
+    assert torch.equal(mf_a.flat_params(), mf_b.flat_params())
+    # the pose gradient is scattered with float atomics (order varies run to run): ulps
+    assert (cam_a.translation_deltas.detach() - cam_b.translation_deltas.detach()).abs().max() < 2e-6
+    assert cam_b.translation_deltas.detach().abs().max() > 1e-6
+    assert opt_p.param_groups[0]["lr"] == trainer.optimizer_poses.param_groups[0]["lr"]
