@@ -61,7 +61,7 @@ def get_rays(directions: torch.Tensor, c2w: torch.Tensor) -> Tuple[torch.Tensor,
 def _pts_bwd(ctx, g_pts, z):
     """pts = o + d * z (rays.py:208 / :331): sum the sample gradients per ray."""
     g_o = g_d = None
-    if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+    if g_pts is not None and (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]):
         B, S = z.shape
         g_o = torch.zeros(B, 3, device=z.device, dtype=_f32) if ctx.needs_input_grad[0] else None
         g_d = torch.zeros(B, 3, device=z.device, dtype=_f32) if ctx.needs_input_grad[1] else None
@@ -81,6 +81,7 @@ class _Stratified(torch.autograd.Function):
              num_samples, ptr(z), ptr(pts), _stream())
         ctx.save_for_backward(z)
         ctx.mark_non_differentiable(z)
+        ctx.set_materialize_grads(False)  # no zero-filled dL/dz launch per step
         return pts, z
 
     @staticmethod
@@ -122,6 +123,7 @@ class _Hierarchical(torch.autograd.Function):
              ptr(zf), ptr(pts), _stream())
         ctx.save_for_backward(zf)
         ctx.mark_non_differentiable(zf)
+        ctx.set_materialize_grads(False)
         return pts, zf
 
     @staticmethod
@@ -210,6 +212,9 @@ class _Composite(torch.autograd.Function):
              ptr(depth), ptr(acc), ptr(weights), _stream())
         ctx.save_for_backward(rgb, sigma, z, rd, nz)
         ctx.white = white
+        # unused outputs (depth/acc in training, the coarse weights) reach backward as
+        # None, which the kernel reads as zero: no zero-filled tensors launched per step
+        ctx.set_materialize_grads(False)
         return rgb_map, depth, acc, weights
 
     @staticmethod
