@@ -64,12 +64,21 @@ int nr_rays_from_pixels_fwd(const int64_t* img_idx, const float* pix,
                             float focal, int B, float* rays_o, float* rays_d,
                             nr_stream_t stream);
 /* Backward: g_poses (n_img,4,4) must be zeroed by the caller; it receives
- * dL/dposes summed over the pixels of each image (g_rays_d nullable). */
+ * dL/dposes summed over the pixels of each image (g_rays_d nullable).  One
+ * workgroup per image sums its rays in a fixed order: no atomics, the result is
+ * bit-identical from run to run.  Rays whose img_idx is outside [0, n_img)
+ * contribute nothing (the forward writes NaN rays for them); callers that take
+ * indices from outside validate them with nr_check_index_range.            */
 int nr_rays_from_pixels_bwd(const int64_t* img_idx, const float* pix,
                             const float* poses, int n_img, int H, int W,
                             float focal, int B, const float* g_rays_o,
                             const float* g_rays_d, float* g_poses,
                             nr_stream_t stream);
+/* flag[0] = 1 if any idx[i] (i < n) lies outside [0, limit); flag untouched
+ * otherwise (caller zeroes it).  Validation for host wrappers that receive
+ * indices from a user (the reference raises IndexError on them).            */
+int nr_check_index_range(const int64_t* idx, int n, int limit, int* flag,
+                         nr_stream_t stream);
 
 /* ---- A4: CameraPoseParameters.get_poses  (noisy_src/train_pose_opt.py:122-226)
  * poses_out[i] = [[R_delta(rot[idx_i]) @ R_init[idx_i], t_init[idx_i] + trans[idx_i]],
@@ -78,12 +87,14 @@ int nr_rays_from_pixels_bwd(const int64_t* img_idx, const float* pix,
 int nr_se3_poses_fwd(const float* init_poses, const float* rot_deltas,
                      const float* trans_deltas, const int64_t* indices, int n,
                      float* poses_out, nr_stream_t stream);
-/* Backward of the above.  g_rot / g_trans are ACCUMULATED (indices may repeat);
- * the caller zeroes them.  At theta < 1e-6 dL/drot is exactly 0, as in the
+/* Backward of the above.  g_rot / g_trans (n_poses,3) are ACCUMULATED (indices
+ * may repeat; each pose sums its rows in row order, deterministically); the
+ * caller zeroes them.  At theta < 1e-6 dL/drot is exactly 0, as in the
  * reference (the torch.where blocks the gradient). fixed_small_angle != 0
  * selects the first-order small-angle Jacobian instead (non-default flag).  */
 int nr_se3_poses_bwd(const float* init_poses, const float* rot_deltas,
-                     const int64_t* indices, int n, const float* g_poses,
+                     const int64_t* indices, int n, int n_poses,
+                     const float* g_poses,
                      int fixed_small_angle, float* g_rot, float* g_trans,
                      nr_stream_t stream);
 
@@ -198,8 +209,13 @@ int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M,
                            nr_stream_t stream);
 
 /* ---- A13: optimizer tail  (noisy_src/train.py:112-117, train_pose_opt.py:398-409)
- * Sum of squares of n fp32 values added into *acc (device scalar, caller-zeroed). */
-int nr_sumsq(const float* x, int64_t n, float* acc, nr_stream_t stream);
+ * Sum of squares of n fp32 values added into *acc (device scalar, caller-zeroed):
+ * the squared global norm of torch.nn.utils.clip_grad_norm_.  A fixed-shape
+ * two-pass reduction (deterministic) through nr_sumsq_workspace_bytes() of
+ * caller-owned scratch; calls on one stream may share the scratch.          */
+int64_t nr_sumsq_workspace_bytes(void);
+int nr_sumsq(const float* x, int64_t n, float* acc, void* workspace,
+             nr_stream_t stream);
 /* torch.optim.Adam (amsgrad=False, maximize=False, weight_decay=0) on a flat
  * buffer: grads are first scaled by clip = min(1, max_norm / (sqrt(*sumsq)
  * + 1e-6)) when sumsq != NULL (torch.nn.utils.clip_grad_norm_), lr is read

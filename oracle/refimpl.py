@@ -461,3 +461,105 @@ def bf16_operand_nerf(model: "NeRF", dtype=torch.bfloat16) -> "NeRF":
 
 def fp16_operand_nerf(model: "NeRF") -> "NeRF":
     return bf16_operand_nerf(model, torch.float16)
+
+
+# --------------------------------------------------------------------------
+# Exact numerics model of the 16-bit MFMA path (parity reference at full size)
+# --------------------------------------------------------------------------
+class _GradRound(torch.autograd.Function):
+    """Identity forward; the backward rounds the gradient to the 16-bit storage type
+    (after scaling by ``scale``, a power of two, as the fp16 path does)."""
+
+    @staticmethod
+    def forward(ctx, z, dtype, scale):
+        ctx.dtype, ctx.scale = dtype, scale
+        return z.view_as(z)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g * ctx.scale).to(ctx.dtype).float() / ctx.scale, None, None
+
+
+class _FwdRound(torch.autograd.Function):
+    """Round to the 16-bit operand type in the forward; the gradient passes through in
+    fp32 untouched (a plain ``x.to(dt).float()`` would round the gradient too)."""
+
+    @staticmethod
+    def forward(ctx, x, dtype):
+        return x.to(dtype).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+class _HeadLinear(torch.autograd.Function):
+    """A head layer (sigma, rgb): fp32 forward on the fp32 activations; backward
+    dx = g W (fp32 g and W), dW = round16(g)^T round16(x), db = sum round16(g)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, dtype, scale):
+        ctx.save_for_backward(x, weight)
+        ctx.dtype, ctx.scale = dtype, scale
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        gr = (g * ctx.scale).to(ctx.dtype).float() / ctx.scale
+        xr = x.to(ctx.dtype).float()
+        return g @ weight, gr.t() @ xr, gr.sum(0), None, None
+
+
+class MfmaEmulatedNeRF(nn.Module):
+    """The NeRF forward/backward of the 16-bit MFMA kernels (csrc/mlp.hip), modelled
+    value by value so that a comparison with them differs only in summation order:
+
+    * every MFMA layer (trunk, feature, dir) takes 16-bit operands (activations and
+      weights) with fp32 accumulation and an fp32 bias;
+    * the sigma and rgb heads run in fp32 on the fp32 activations (VALU);
+    * backward: each layer's dz (after its ReLU mask) is stored in 16 bit -- scaled by
+      ``grad_scale`` (2^14 on the fp16 path) -- and both dX = W^T dz and dW = dz^T x use
+      the stored value; the heads' dz feed dX in fp32 and dW in 16 bit, against the
+      16-bit saved activations.
+
+    Shares the base model's parameters (gradients land in them).  This models the
+    build's arithmetic; the reference semantics it rounds are those of ``NeRF`` above."""
+
+    def __init__(self, base: "NeRF", dtype=torch.bfloat16, grad_scale: float = 1.0):
+        super().__init__()
+        self.base = base
+        self.dtype = dtype
+        self.scale = float(grad_scale)
+
+    def _lin(self, x, lin):
+        dt = self.dtype
+        return F.linear(_FwdRound.apply(x, dt), _FwdRound.apply(lin.weight, dt), lin.bias)
+
+    def forward(self, x, d=None):
+        b, dt, s = self.base, self.dtype, self.scale
+        x_enc = b.pos_encoder(x)
+        h = x_enc
+        for i, layer in enumerate(b.pts_linears):
+            h = F.relu(_GradRound.apply(self._lin(h, layer), dt, s))
+            if i in b.config.skips:
+                h = torch.cat([x_enc, h], dim=-1)
+        sigma = F.relu(_HeadLinear.apply(h, b.sigma_linear.weight, b.sigma_linear.bias, dt, s))
+        feats = _GradRound.apply(self._lin(h, b.feature_linear), dt, s)
+        if b.config.use_view_dirs and d is not None:
+            h_color = torch.cat([feats, b.dir_encoder(d)], dim=-1)
+        else:
+            h_color = feats
+        h_color = F.relu(_GradRound.apply(self._lin(h_color, b.dir_linear), dt, s))
+        rgb = torch.sigmoid(_HeadLinear.apply(h_color, b.rgb_linear.weight, b.rgb_linear.bias, dt, s))
+        return rgb, sigma
+
+
+def mfma_emulated_nerf(model: "NeRF", precision: str) -> nn.Module:
+    """The exact numerics model for ModelConfig.precision 'bf16' or 'fp16' (fp16 backward
+    on dz scaled by 2^14, include/nerf_hip.h NR_PREC_FP16)."""
+    if precision == "bf16":
+        return MfmaEmulatedNeRF(model, torch.bfloat16, 1.0)
+    if precision == "fp16":
+        return MfmaEmulatedNeRF(model, torch.float16, 2.0 ** 14)
+    raise ValueError(precision)

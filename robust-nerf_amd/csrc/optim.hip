@@ -7,32 +7,50 @@
 //       m.lerp_(g, 1-b1); v = b2 v + (1-b2) g^2; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
 //   LambdaLR 0.1^(step/250000)                          noisy_src/train.py:405-411 (host)
 // HBM-bound: ~20 B read + 16 B written per parameter; 16-B vector accesses.
+//
+// Determinism: the sum of squares is a fixed-shape two-pass reduction (a constant
+// grid of kSumsqBlocks partials, then one block that sums them in index order), so
+// the clip coefficient — and with it every data-parallel replica's Adam update — is
+// bit-identical from run to run (the reference is bit-deterministic).
 #include <cmath>
 
 #include "common.hpp"
 
 namespace nr {
 
-__global__ void sumsq_kernel(const float* x, int64_t n, float* acc) {
+constexpr int kSumsqBlocks = 256;
+constexpr int kSumsqThreads = 256;
+static_assert(kSumsqBlocks == kSumsqThreads, "the final pass reads one partial per thread");
+
+// Sum of a block's values in a fixed order: wave butterfly, then waves in index order.
+__device__ __forceinline__ float block_sum_fixed(float s) {
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    __shared__ float part[kSumsqThreads / 64];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    float t = 0.f;
+    for (int i = 0; i < kSumsqThreads / 64; ++i) t += part[i];
+    return t;
+}
+
+__global__ void __launch_bounds__(kSumsqThreads) sumsq_partial_kernel(const float* x, int64_t n, float* partials) {
     float s = 0.f;
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    const int64_t stride = static_cast<int64_t>(kSumsqBlocks) * kSumsqThreads;
     const int64_t n4 = n / 4;
     const float4* x4 = reinterpret_cast<const float4*>(x);
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kSumsqThreads + threadIdx.x; i < n4; i += stride) {
         const float4 v = x4[i];
         s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
     }
-    for (int64_t i = 4 * n4 + static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+    for (int64_t i = 4 * n4 + static_cast<int64_t>(blockIdx.x) * kSumsqThreads + threadIdx.x; i < n; i += stride)
         s += x[i] * x[i];
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    __shared__ float part[16];
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float t = 0.f;
-        for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) t += part[i];
-        atomicAdd(acc, t);
-    }
+    const float t = block_sum_fixed(s);
+    if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+__global__ void __launch_bounds__(kSumsqThreads) sumsq_final_kernel(const float* partials, float* acc) {
+    const float t = block_sum_fixed(partials[threadIdx.x]);
+    if (threadIdx.x == 0) *acc += t;
 }
 
 __device__ __forceinline__ void adam_one(float& p, float& g, float& m, float& v, float coef, float omb1, float b2,
@@ -80,12 +98,18 @@ using namespace nr;
 
 extern "C" {
 
-int nr_sumsq(const float* x, int64_t n, float* acc, nr_stream_t stream) {
-    NR_REQUIRE(x && acc && n >= 0, "nr_sumsq: bad arguments");
+int64_t nr_sumsq_workspace_bytes(void) { return static_cast<int64_t>(kSumsqBlocks) * sizeof(float); }
+
+int nr_sumsq(const float* x, int64_t n, float* acc, void* workspace, nr_stream_t stream) {
+    NR_REQUIRE(x && acc && workspace && n >= 0, "nr_sumsq: bad arguments");
     NR_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0, "nr_sumsq: x must be 16-byte aligned");
     if (n == 0) return NR_OK;
-    const int grid = stream_grid(ceil_div_ll(n, 4), 256) > 512 ? 512 : stream_grid(ceil_div_ll(n, 4), 256);
-    hipLaunchKernelGGL(sumsq_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), x, n, acc);
+    float* partials = static_cast<float*>(workspace);
+    hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kSumsqBlocks), dim3(kSumsqThreads), 0,
+                       static_cast<hipStream_t>(stream), x, n, partials);
+    NR_LAUNCH_CHECK("nr_sumsq");
+    hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(kSumsqThreads), 0, static_cast<hipStream_t>(stream),
+                       partials, acc);
     NR_LAUNCH_CHECK("nr_sumsq");
     return NR_OK;
 }

@@ -59,7 +59,8 @@ _SIGNATURES = {
     "nr_rays_from_pixels_fwd": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_i, c_f, c_i, c_vp, c_vp, c_vp]),
     "nr_rays_from_pixels_bwd": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_i, c_f, c_i, c_vp, c_vp, c_vp, c_vp]),
     "nr_se3_poses_fwd": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_vp, c_vp]),
-    "nr_se3_poses_bwd": (c_i, [c_vp, c_vp, c_vp, c_i, c_vp, c_i, c_vp, c_vp, c_vp]),
+    "nr_check_index_range": (c_i, [c_vp, c_i, c_i, c_vp, c_vp]),
+    "nr_se3_poses_bwd": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_vp, c_i, c_vp, c_vp, c_vp]),
     "nr_stratified_sample": (c_i, [c_vp, c_vp, c_vp, c_f, c_f, c_i, c_i, c_i, c_vp, c_vp, c_vp]),
     "nr_positional_encoding": (c_i, [c_vp, c_i64, c_i, c_i, c_i, c_i, c_vp, c_vp]),
     "nr_positional_encoding_bwd": (c_i, [c_vp, c_i64, c_i, c_i, c_i, c_i, c_vp, c_vp, c_vp]),
@@ -80,7 +81,8 @@ _SIGNATURES = {
                                  c_vp, c_vp]),
     "nr_mlp_backward_dw": (c_i, [_cfg_p, c_i64, c_vp, c_vp, c_vp]),
     "nr_mlp_backward_reduce": (c_i, [_cfg_p, c_i64, c_vp, c_vp, c_vp]),
-    "nr_sumsq": (c_i, [c_vp, c_i64, c_vp, c_vp]),
+    "nr_sumsq_workspace_bytes": (c_i64, []),
+    "nr_sumsq": (c_i, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "nr_adam_step": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_d, c_d, c_d, c_d, c_i64, c_vp, c_f, c_vp]),
     "nr_expand_viewdirs": (c_i, [c_vp, c_i, c_i, c_vp, c_vp]),
     "nr_pts_bwd": (c_i, [c_vp, c_vp, c_i, c_i, c_vp, c_vp, c_vp]),

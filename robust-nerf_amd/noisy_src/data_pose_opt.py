@@ -28,10 +28,13 @@ class PixelBatch:
     image_indices: torch.Tensor  # (B,) int64
     pixel_coords: torch.Tensor   # (B, 2) float (u, v)
     target_rgb: torch.Tensor     # (B, 3)
+    # set by PixelSampler.sample_batch, whose indices are in range by construction;
+    # batches built elsewhere are validated (one host sync) before the ray kernel
+    in_range: bool = False
 
     def slice(self, sl: slice) -> "PixelBatch":
         """Rows ``sl`` of the batch (a data-parallel rank's contiguous share)."""
-        return PixelBatch(self.image_indices[sl], self.pixel_coords[sl], self.target_rgb[sl])
+        return PixelBatch(self.image_indices[sl], self.pixel_coords[sl], self.target_rgb[sl], self.in_range)
 
 
 class PixelDataset:
@@ -57,7 +60,8 @@ class PixelDataset:
         uniq, inv = torch.unique(pixel_batch.image_indices, return_inverse=True)
         if poses.shape[0] != uniq.shape[0]:
             raise ValueError(f"get_rays_from_pixels: {poses.shape[0]} poses for {uniq.shape[0]} unique images")
-        return ops.rays_from_pixels(inv, pixel_batch.pixel_coords, poses, self.H, self.W, self.focal)
+        return ops.rays_from_pixels(inv, pixel_batch.pixel_coords, poses, self.H, self.W, self.focal,
+                                    validate=not pixel_batch.in_range)
 
 
 class PixelSampler:
@@ -75,14 +79,15 @@ class PixelSampler:
         idx = torch.randint(0, self.n_pixels, (self.batch_size,), device=self.device, generator=generator)
         ds = self.dataset
         return PixelBatch(image_indices=ds.image_indices[idx], pixel_coords=ds.pixel_coords[idx],
-                          target_rgb=ds.target_rgb[idx])
+                          target_rgb=ds.target_rgb[idx], in_range=True)
 
     def get_rays_for_batch(self, pixel_batch: PixelBatch, poses: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """Reference data_pose_opt.py:200-223 with ``poses`` = every image's pose (N,4,4):
         the kernel indexes them by image directly (the reference's unique/select/loop
         gives the same rays), and the pose gradient lands on every image in the batch."""
         ds = self.dataset
-        return ops.rays_from_pixels(pixel_batch.image_indices, pixel_batch.pixel_coords, poses, ds.H, ds.W, ds.focal)
+        return ops.rays_from_pixels(pixel_batch.image_indices, pixel_batch.pixel_coords, poses, ds.H, ds.W, ds.focal,
+                                    validate=not pixel_batch.in_range)
 
 
 def create_pixel_dataset(data: BlenderData) -> Tuple[PixelDataset, PixelSampler]:

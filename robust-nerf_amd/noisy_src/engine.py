@@ -22,6 +22,49 @@ from .optim import FusedAdam
 from .rendering import render_rays
 
 
+def init_distributed(device: str = "cuda"):
+    """One process per GPU under ``torch.distributed.run``: reads RANK / LOCAL_RANK /
+    WORLD_SIZE, binds the local GPU and joins the default group (backend "nccl" = RCCL
+    on ROCm; "gloo" for CPU-device runs).  Returns (process_group or None, rank, world,
+    device string).  Without the torchrun environment it is a single process."""
+    import os
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if device.startswith("cuda") and torch.cuda.is_available():
+        # one GPU per rank; ranks beyond the visible GPUs share them (gloo test mode)
+        local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        device = f"cuda:{local}"
+    if world <= 1:
+        return None, 0, 1, device
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        if device.startswith("cuda") and os.environ.get("NR_DIST_BACKEND", "nccl") == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(device))
+        else:
+            dist.init_process_group("gloo")
+    return dist.group.WORLD, rank, world, device
+
+
+def rank_slice(n_global: int, rank: int, world: int) -> slice:
+    """Rank r's contiguous share [r*B/N, (r+1)*B/N) of a global batch."""
+    if n_global % world:
+        raise ValueError(f"global batch {n_global} is not divisible by world size {world}")
+    per = n_global // world
+    return slice(rank * per, (rank + 1) * per)
+
+
+def mean_over_ranks(values, process_group=None):
+    """Average a list of device scalars over the group (the logged global-batch losses)."""
+    t = torch.stack([v.detach().float().reshape(()) for v in values])
+    if process_group is not None:
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=process_group)
+        t = t / dist.get_world_size(process_group)
+    return t
+
+
 def lr_lambda_factory(lr_decay: int):
     decay_steps = lr_decay * 1000
 
@@ -113,8 +156,14 @@ class PoseTrainer:
     into the Adams, the pose Adam and its LambdaLR only once ``optimize_poses``.  The
     reference's ``.item()`` metrics are left to the caller (losses stay on the device).
     Data parallel: the network gradients all-reduce as in ``Trainer``; the pose gradient
-    (each rank touches its own images) is one more all-reduce of 2 x 3 x n_poses floats,
-    whose SUM over ranks is the single-process gradient."""
+    (each rank touches its own images) is one more all-reduce of 2 x 3 x n_poses floats.
+    Every gradient is AVERAGED over the ranks: each rank's loss is the mean over its
+    equal share of the global batch plus the replicated pose regulariser, so the mean
+    of the rank gradients is the single-process gradient.
+    Before the pose-optimisation delay (``optimize_poses=False``) the poses enter the
+    step detached: the reference lets their gradient accumulate unused until the first
+    optimising step's ``zero_grad``, so skipping it changes
+    nothing and saves the MLP's input-gradient pass."""
 
     def __init__(self, model_coarse, model_fine, camera_params, pixel_sampler, render_config,
                  lr: float = 5e-4, pose_lr: float = 1e-4, lr_decay: int = 250,
@@ -145,7 +194,10 @@ class PoseTrainer:
         self.optimizer_nerf.zero_grad(set_to_none=True)
         if optimize_poses:
             self.optimizer_poses.zero_grad(set_to_none=True)
-        rays_o, rays_d = self.pixel_sampler.get_rays_for_batch(pixel_batch, cam.get_all_poses())
+        poses = cam.get_all_poses()
+        if not optimize_poses:
+            poses = poses.detach()
+        rays_o, rays_d = self.pixel_sampler.get_rays_for_batch(pixel_batch, poses)
         target = pixel_batch.target_rgb
         out = render_rays(self.model_coarse, self.model_fine, rays_o, rays_d, self.render_config, is_train=True,
                           t_rand=t_rand, u=u)

@@ -38,6 +38,8 @@ def load_checkpoint(checkpoint_path: Path, device: str = "cuda") -> tuple:
     ckpt = torch.load(checkpoint_path, map_location=device, weights_only=True)
     cfg = ckpt.get("config", {})
     model_cfg = ModelConfig(**cfg.get("model", {}))
+    # MI355X-only knob, kept out of config["model"] so reference loaders accept the file
+    model_cfg.precision = ckpt.get("mi355x", {}).get("precision", model_cfg.precision)
     render_cfg = RenderConfig(**cfg.get("render", {}))
     coarse = NeRF(model_cfg).to(device)
     coarse.load_state_dict(ckpt["model_coarse"])

@@ -1,16 +1,19 @@
 """
-Experiment logging — the reference's metric containers and CSV schema
-(ShawnnnLiu/Robust-NeRF ``noisy_src/logger.py:26-156``), so output folders stay
-comparable with the reference's ``outputs/*/train_metrics.csv`` / ``val_metrics.csv``.
-TensorBoard is optional in the reference and not installed here; ``ExperimentLogger``
-writes the CSVs, the config/summary JSON and PNG previews.
+Experiment logging — the reference's metric containers, CSV schema and output layout
+(ShawnnnLiu/Robust-NeRF ``noisy_src/logger.py:26-368``), so output folders stay
+comparable with the reference's ``outputs/<exp>/``: ``config.json``, ``summary.json``,
+``logs/train_metrics.csv`` (one row per iteration, flushed), ``logs/val_metrics.csv``,
+``images/{tag}_{pred,gt,comparison,depth}_{iteration:07d}.png``.  TensorBoard is optional
+in the reference and not installed here, so that backend reports itself unavailable.
 """
 
 from __future__ import annotations
 
 import csv
 import json
-from dataclasses import asdict, dataclass, field, is_dataclass
+import time
+from dataclasses import asdict, dataclass, field
+from datetime import datetime
 from pathlib import Path
 from typing import Any, Dict, List, Optional
 
@@ -51,6 +54,28 @@ class ValidationMetrics:
         return {k: v for k, v in asdict(self).items() if v is not None and v != []}
 
 
+class TensorBoardLogger:
+    """Reference logger.py:60-108.  ``tensorboard`` is not installed in this image, so
+    ``available`` is False and every call is a no-op, as in the reference without it."""
+
+    def __init__(self, log_dir: Path):
+        self.writer = None
+        try:  # pragma: no cover - optional dependency
+            from torch.utils.tensorboard import SummaryWriter
+            self.writer = SummaryWriter(str(log_dir))
+        except Exception:
+            self.writer = None
+        self.available = self.writer is not None
+
+    def log_scalar(self, tag: str, value: float, step: int) -> None:
+        if self.available:
+            self.writer.add_scalar(tag, value, step)
+
+    def close(self) -> None:
+        if self.writer is not None:
+            self.writer.close()
+
+
 class CSVLogger:
     """Reference logger.py:111-156: header from the first row's keys, flushed per row."""
 
@@ -83,53 +108,106 @@ class CSVLogger:
         self._w.clear()
 
 
-class ExperimentLogger:
-    """Reference logger.py:159-368 (CSV + JSON + PNG parts)."""
+def _save_png(img: torch.Tensor, path: Path) -> None:
+    from PIL import Image
+    arr = (img.detach().float().cpu().numpy() * 255).clip(0, 255).astype(np.uint8)
+    Image.fromarray(arr).save(path)
 
-    def __init__(self, output_dir: Path, experiment_name: str, use_tensorboard: bool = False):
+
+def depth_to_colormap(depth: torch.Tensor) -> torch.Tensor:
+    """Reference logger.py:290-302: min-max normalised depth through a turbo-like ramp."""
+    depth = depth.detach().float().cpu()
+    n = (depth - depth.min()) / (depth.max() - depth.min() + 1e-8)
+    return torch.stack([torch.clamp(4 * n - 1.5, 0, 1), torch.clamp(2 - 4 * torch.abs(n - 0.5), 0, 1),
+                        torch.clamp(1.5 - 4 * n, 0, 1)], dim=-1)
+
+
+class ExperimentLogger:
+    """Reference logger.py:159-368: CSVs under ``logs/``, PNGs under ``images/``,
+    ``config.json`` and a ``summary.json`` of run metadata and final/best metrics."""
+
+    def __init__(self, output_dir: Path, experiment_name: str = "experiment", use_tensorboard: bool = True):
         self.output_dir = Path(output_dir)
         self.experiment_name = experiment_name
         self.output_dir.mkdir(parents=True, exist_ok=True)
-        (self.output_dir / "images").mkdir(exist_ok=True)
-        self.csv = CSVLogger(self.output_dir)
-        self.train_history: List[Dict[str, Any]] = []
-        self.val_history: List[Dict[str, Any]] = []
+        self.logs_dir = self.output_dir / "logs"
+        self.images_dir = self.output_dir / "images"
+        self.logs_dir.mkdir(exist_ok=True)
+        self.images_dir.mkdir(exist_ok=True)
+        self.csv_logger = CSVLogger(self.logs_dir)
+        self.tb_logger = TensorBoardLogger(self.logs_dir / "tensorboard") if use_tensorboard else None
+        self.train_history: List[TrainingMetrics] = []
+        self.val_history: List[ValidationMetrics] = []
+        self.start_time = time.time()
+        self.metadata: Dict[str, Any] = {"experiment_name": experiment_name, "start_time": datetime.now().isoformat(),
+                                         "output_dir": str(output_dir)}
 
     def log_training(self, metrics: TrainingMetrics) -> None:
-        self.csv.log_train(metrics)
-        self.train_history.append(metrics.to_dict())
+        self.train_history.append(metrics)
+        self.csv_logger.log_train(metrics)
+        if self.tb_logger is not None and self.tb_logger.available:
+            for k in ("loss", "loss_coarse", "loss_fine", "psnr", "learning_rate", "rays_per_sec"):
+                v = getattr(metrics, k)
+                if v is not None:
+                    self.tb_logger.log_scalar(f"train/{k}", v, metrics.iteration)
 
     def log_validation(self, metrics: ValidationMetrics) -> None:
-        self.csv.log_val(metrics)
-        self.val_history.append(metrics.to_dict())
+        self.val_history.append(metrics)
+        self.csv_logger.log_val(metrics)
+        if self.tb_logger is not None and self.tb_logger.available:
+            for k in ("psnr", "ssim", "mse", "lpips"):
+                v = getattr(metrics, k)
+                if v is not None:
+                    self.tb_logger.log_scalar(f"val/{k}", v, metrics.iteration)
 
-    def log_images(self, tag: str, pred: torch.Tensor, gt: Optional[torch.Tensor] = None, iteration: int = 0,
+    def log_images(self, tag: str, pred: torch.Tensor, gt: torch.Tensor, iteration: int,
                    depth: Optional[torch.Tensor] = None) -> None:
-        self._save_image(pred, self.output_dir / "images" / f"{tag}_pred_{iteration:06d}.png")
-        if gt is not None:
-            self._save_image(gt, self.output_dir / "images" / f"{tag}_gt_{iteration:06d}.png")
+        """Reference logger.py:242-281 (pred, gt, side-by-side comparison, depth)."""
+        _save_png(pred, self.images_dir / f"{tag}_pred_{iteration:07d}.png")
+        _save_png(gt, self.images_dir / f"{tag}_gt_{iteration:07d}.png")
+        _save_png(torch.cat([gt.detach().float().cpu(), pred.detach().float().cpu()], dim=1),
+                  self.images_dir / f"{tag}_comparison_{iteration:07d}.png")
+        if depth is not None:
+            _save_png(depth_to_colormap(depth), self.images_dir / f"{tag}_depth_{iteration:07d}.png")
 
-    def _save_image(self, img: torch.Tensor, path: Path) -> None:
-        from PIL import Image
-        arr = (img.detach().float().clamp(0, 1).cpu().numpy() * 255).astype(np.uint8)
-        Image.fromarray(arr).save(path)
+    def log_model_info(self, model: torch.nn.Module, name: str = "model") -> None:
+        """Reference logger.py:304-313."""
+        total = sum(p.numel() for p in model.parameters())
+        trainable = sum(p.numel() for p in model.parameters() if p.requires_grad)
+        self.metadata[f"{name}_total_params"] = total
+        self.metadata[f"{name}_trainable_params"] = trainable
+        print(f"{name}: {total:,} total params, {trainable:,} trainable")
 
     def log_config(self, config: Any) -> None:
-        (self.output_dir / "config.json").write_text(json.dumps(self._config_to_dict(config), indent=2, default=str))
+        cfg = self._config_to_dict(config) if hasattr(config, "__dict__") else config
+        self.metadata["config"] = cfg
+        (self.output_dir / "config.json").write_text(json.dumps(cfg, indent=2, default=str))
 
     def _config_to_dict(self, obj: Any) -> Any:
-        if is_dataclass(obj):
-            return {k: self._config_to_dict(v) for k, v in asdict(obj).items()}
+        if hasattr(obj, "__dataclass_fields__"):
+            return {k: self._config_to_dict(v) for k, v in obj.__dict__.items()}
+        if isinstance(obj, Path):
+            return str(obj)
+        if isinstance(obj, (list, tuple)):
+            return [self._config_to_dict(v) for v in obj]
         return obj
 
     def save_summary(self) -> None:
-        summary = {"experiment_name": self.experiment_name, "total_iterations": len(self.train_history)}
+        """Reference logger.py:338-363."""
+        self.metadata["end_time"] = datetime.now().isoformat()
+        self.metadata["total_time_seconds"] = time.time() - self.start_time
+        self.metadata["total_iterations"] = len(self.train_history)
         if self.val_history:
-            best = max(self.val_history, key=lambda m: m.get("psnr", float("-inf")))
-            summary["best_psnr"] = best.get("psnr")
-            summary["final_psnr"] = self.val_history[-1].get("psnr")
-        (self.output_dir / "summary.json").write_text(json.dumps(summary, indent=2))
+            final = self.val_history[-1]
+            self.metadata["final_val_psnr"] = final.psnr
+            self.metadata["final_val_ssim"] = final.ssim
+            if final.lpips:
+                self.metadata["final_val_lpips"] = final.lpips
+            self.metadata["best_val_psnr"] = max(v.psnr for v in self.val_history)
+            self.metadata["best_val_ssim"] = max(v.ssim for v in self.val_history)
+        (self.output_dir / "summary.json").write_text(json.dumps(self.metadata, indent=2, default=str))
 
     def close(self) -> None:
-        self.save_summary()
-        self.csv.close()
+        self.csv_logger.close()
+        if self.tb_logger is not None:
+            self.tb_logger.close()

@@ -267,9 +267,24 @@ class _RaysFromPixels(torch.autograd.Function):
         return None, None, g_poses, None, None, None
 
 
-def rays_from_pixels(img_idx, pix, poses, H, W, focal):
-    """get_rays_from_pixels (data_pose_opt.py:83-148) in one pass; poses indexed by img_idx."""
+def check_index_range(idx: torch.Tensor, limit: int, what: str = "index") -> None:
+    """Raise IndexError (as torch indexing in the reference would) if any idx is outside
+    [0, limit).  One device kernel plus one host read of the flag."""
+    _check(idx)
+    i = idx.to(torch.int64).contiguous()
+    flag = torch.zeros(1, device=i.device, dtype=torch.int32)
+    call("nr_check_index_range", ptr(i), i.numel(), int(limit), ptr(flag), _stream())
+    if int(flag.item()):
+        raise IndexError(f"{what} out of range for {limit} entries")
+
+
+def rays_from_pixels(img_idx, pix, poses, H, W, focal, validate: bool = False):
+    """get_rays_from_pixels (data_pose_opt.py:83-148) in one pass; poses indexed by img_idx.
+    ``validate`` checks img_idx against poses.shape[0] first (IndexError); unchecked
+    out-of-range rays come out NaN and get no pose gradient."""
     _check(img_idx, pix, poses)
+    if validate:
+        check_index_range(img_idx, poses.shape[0], "image index")
     return _RaysFromPixels.apply(img_idx, pix, poses, H, W, focal)
 
 
@@ -293,8 +308,8 @@ class _Se3Poses(torch.autograd.Function):
         has_r, has_t, has_idx, n, fixed = ctx.flags
         g_rot = torch.zeros(ini.shape[0], 3, device=ini.device, dtype=_f32) if (has_r and ctx.needs_input_grad[1]) else None
         g_trans = torch.zeros(ini.shape[0], 3, device=ini.device, dtype=_f32) if (has_t and ctx.needs_input_grad[2]) else None
-        call("nr_se3_poses_bwd", ptr(ini), ptr(r) if has_r else None, ptr(idx) if has_idx else None, n, ptr(_c(g)),
-             int(fixed), ptr(g_rot), ptr(g_trans), _stream())
+        call("nr_se3_poses_bwd", ptr(ini), ptr(r) if has_r else None, ptr(idx) if has_idx else None, n,
+             ini.shape[0], ptr(_c(g)), int(fixed), ptr(g_rot), ptr(g_trans), _stream())
         return None, g_rot, g_trans, None, None
 
 
@@ -315,8 +330,16 @@ def mse_loss_and_grad(pred, target, scale=1.0):
 
 
 # ---------------------------------------------------------------- optimizer --
+_sumsq_ws = {}
+
+
 def sumsq_into(x: torch.Tensor, acc: torch.Tensor) -> None:
-    call("nr_sumsq", ptr(x), x.numel(), ptr(acc), _stream())
+    """acc += sum(x^2) (fixed-order two-pass reduction: bit-reproducible)."""
+    ws = _sumsq_ws.get(x.device)
+    if ws is None:
+        ws = torch.empty(int(_hip.load().nr_sumsq_workspace_bytes()), device=x.device, dtype=torch.uint8)
+        _sumsq_ws[x.device] = ws  # stream-ordered reuse: every call runs on the current stream
+    call("nr_sumsq", ptr(x), x.numel(), ptr(acc), ptr(ws), _stream())
 
 
 def adam_step(p, g, m, v, lr, beta1, beta2, eps, step, sumsq=None, max_norm=1.0):

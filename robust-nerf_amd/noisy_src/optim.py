@@ -82,9 +82,26 @@ class FusedAdam(torch.optim.Optimizer):
     group into the update (train.py:115 joint clip; train_pose_opt.py:398-404
     per-network clips)."""
 
-    def __init__(self, params, lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999), eps: float = 1e-8):
-        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+    def __init__(self, params, lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, amsgrad: bool = False, *, maximize: bool = False, foreach=None,
+                 capturable: bool = False, differentiable: bool = False, fused=None,
+                 decoupled_weight_decay: bool = False):
+        # the reference's Adam (train.py:402, train_pose_opt.py:788-789) uses the defaults;
+        # the fused kernel implements exactly that configuration
+        if weight_decay != 0.0 or amsgrad or maximize or differentiable or decoupled_weight_decay:
+            raise ValueError("FusedAdam implements torch.optim.Adam with weight_decay=0, amsgrad=False, "
+                             "maximize=False, differentiable=False only")
+        # the full torch.optim.Adam param-group keys, so state_dict() loads into torch's Adam
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0.0, amsgrad=False,
+                                      maximize=False, foreach=foreach, capturable=capturable,
+                                      differentiable=False, fused=fused, decoupled_weight_decay=False))
         self._flat_state = {}
+
+    def load_state_dict(self, state_dict) -> None:
+        """torch's load, then drop the flat m/v buffers so the next step adopts the loaded
+        exp_avg / exp_avg_sq (instead of updating stale buffers)."""
+        super().load_state_dict(state_dict)
+        self._flat_state.clear()
 
     def _state_run(self, run: List[torch.nn.Parameter]):
         key = tuple(id(p) for p in run)

@@ -1,19 +1,35 @@
 """
-NeRF training step and image rendering — drop-in for ShawnnnLiu/Robust-NeRF
-``noisy_src/train.py`` (the functions on and around the hot path).
+NeRF training entry point — drop-in for ShawnnnLiu/Robust-NeRF ``noisy_src/train.py``.
 
-``train_step(renderer, optimizer, batch)`` keeps the reference's signature and
-returned metrics (train.py:68-119: four host syncs for the logged scalars, joint
-clip at 1.0 over both networks).  With the package's ``FusedAdam`` the clip folds
-into the fused update.  ``engine.Trainer`` is the same step without the host syncs,
-which is what ``bench.py`` times.  ``train`` is a minimal loop over a ``RaySampler``;
-``save_checkpoint`` / ``load_checkpoint`` keep the reference's checkpoint format.
+* ``train_step(renderer, optimizer, batch)`` keeps the reference's signature and
+  returned metrics (train.py:68-119: host syncs for the logged scalars, joint clip at
+  1.0 over both networks).  With the package's ``FusedAdam`` the clip folds into the
+  fused update.
+* ``train(config, noise_config)`` is the reference loop (train.py:307-577): seed,
+  data (optionally with fixed pose noise), both networks, Adam + LambdaLR, one CSV
+  row per iteration, validation + checkpoint every ``val_every`` (``checkpoint_best``
+  on a new best PSNR), a plain checkpoint every ``save_every``, a final checkpoint,
+  the final evaluation on every validation view and ``summary.json``.  The step
+  itself is ``engine.Trainer`` (HIP kernels, no host syncs); the logged scalars are
+  read once per iteration as the reference does.
+* Data parallel (``torchrun --nproc-per-node N -m noisy_src.train ...``): every rank
+  draws the SAME global batch and random numbers (identical seeds), takes its
+  contiguous slice, and the gradients are averaged over RCCL inside
+  the backward; ``--batch_size`` stays the global batch.  Rank 0 logs, validates and
+  writes the checkpoints.
+* ``save_checkpoint`` / ``load_checkpoint`` keep the reference's format; the MI355X
+  precision knob is stored under a separate top-level key so the reference's
+  ``ModelConfig(**cfg["model"])`` still loads the file.
 """
 
 from __future__ import annotations
 
+import json
+import math
 import random
 import time
+from datetime import datetime
+from pathlib import Path
 from typing import Dict, Optional
 
 import numpy as np
@@ -21,10 +37,12 @@ import torch
 
 from . import ops
 from .config import NeRFConfig
-from .data import BlenderData, RayDataset, RaySampler
-from .engine import Trainer, lr_lambda_factory
-from .metrics import compute_mse, compute_psnr, compute_ssim
+from .data import BlenderData, RayDataset, RaySampler, create_data_loaders
+from .engine import Trainer, init_distributed, mean_over_ranks, rank_slice
+from .logger import ExperimentLogger, TrainingMetrics, ValidationMetrics
+from .metrics import LPIPSMetric, compute_mse, compute_psnr, compute_ssim
 from .model import create_nerf
+from .noise import NoiseConfig
 from .optim import FusedAdam, clip_grad_norm_
 from .rays import get_ray_directions, get_rays
 from .rendering import NeRFRenderer
@@ -37,6 +55,13 @@ def set_seed(seed: int) -> None:
     torch.manual_seed(seed)
     if torch.cuda.is_available():
         torch.cuda.manual_seed_all(seed)
+
+
+def generate_experiment_name(scene: str, noise_config: Optional[NoiseConfig], base_name: str = "") -> str:
+    """Reference train.py:44-66: ``{scene}[_{base}]_{noise|clean}_{timestamp}``."""
+    ts = datetime.now().strftime("%Y%m%d_%H%M%S")
+    noise_desc = str(noise_config) if noise_config is not None and noise_config.has_noise else "clean"
+    return f"{scene}_{base_name}_{noise_desc}_{ts}" if base_name else f"{scene}_{noise_desc}_{ts}"
 
 
 def train_step(renderer: NeRFRenderer, optimizer: torch.optim.Optimizer, batch: Dict[str, torch.Tensor],
@@ -76,7 +101,7 @@ def render_image(renderer: NeRFRenderer, pose: torch.Tensor, H: int, W: int, foc
                  chunk_size: int = 1024 * 4) -> Dict[str, torch.Tensor]:
     """Reference train.py:122-160: every pixel of one view, deterministic (is_train=False)."""
     dirs = get_ray_directions(H, W, focal, device=pose.device)
-    rays_o, rays_d = get_rays(dirs, pose.contiguous())
+    rays_o, rays_d = get_rays(dirs, pose.detach().contiguous())
     out = renderer(rays_o.reshape(-1, 3), rays_d.reshape(-1, 3), chunk_size=chunk_size, is_train=False)
     key = "fine" if "rgb_fine" in out else "coarse"
     return {"rgb": out[f"rgb_{key}"].reshape(H, W, 3), "depth": out[f"depth_{key}"].reshape(H, W),
@@ -84,47 +109,65 @@ def render_image(renderer: NeRFRenderer, pose: torch.Tensor, H: int, W: int, foc
 
 
 @torch.no_grad()
-def evaluate(renderer: NeRFRenderer, val_data: BlenderData, num_images: int = 5,
-             chunk_size: int = 1024 * 4) -> Dict[str, object]:
-    """Reference train.py:164-233 without the logger: mean PSNR / SSIM / MSE over the
-    first ``num_images`` validation views."""
-    psnr, ssim, mse = [], [], []
+def evaluate(renderer: NeRFRenderer, val_data: BlenderData, logger: Optional[ExperimentLogger] = None,
+             iteration: int = 0, num_images: int = 5, lpips_metric: Optional[LPIPSMetric] = None,
+             chunk_size: int = 1024 * 4) -> ValidationMetrics:
+    """Reference train.py:163-233: mean PSNR / SSIM / MSE (+ LPIPS when available) over
+    the first ``num_images`` validation views; PNGs of the first three when a logger is
+    given."""
+    psnr, ssim, mse, lp = [], [], [], []
     for i in range(min(num_images, val_data.images.shape[0])):
         out = render_image(renderer, val_data.poses[i], val_data.H, val_data.W, val_data.focal, chunk_size)
         pred, target = out["rgb"], val_data.images[i]
         mse.append(compute_mse(pred, target).item())
         psnr.append(compute_psnr(pred, target).item())
         ssim.append(compute_ssim(pred, target).item())
-    return {"psnr": float(np.mean(psnr)), "ssim": float(np.mean(ssim)), "mse": float(np.mean(mse)),
-            "per_image_psnr": psnr, "per_image_ssim": ssim}
+        if lpips_metric is not None:
+            v = lpips_metric(pred, target)
+            if v is not None:
+                lp.append(v.item())
+        if logger is not None and i < 3:
+            logger.log_images(f"val_{i}", pred, target, iteration, depth=out["depth"])
+    return ValidationMetrics(iteration=iteration, psnr=float(np.mean(psnr)), ssim=float(np.mean(ssim)),
+                             mse=float(np.mean(mse)), lpips=float(np.mean(lp)) if lp else None,
+                             per_image_psnr=psnr, per_image_ssim=ssim)
+
+
+def _plain(d: dict) -> dict:
+    """Config values made plain (Path -> str, tuple -> list) so that the file reads back
+    with ``torch.load(..., weights_only=True)``."""
+    return {k: str(v) if isinstance(v, Path) else list(v) if isinstance(v, tuple) else v for k, v in d.items()}
+
+
+def checkpoint_config(config: NeRFConfig) -> dict:
+    """The reference's ``checkpoint["config"]`` (train.py:256-264).  ``ModelConfig.precision``
+    (an MI355X-only field) is left out so the reference's ``ModelConfig(**cfg["model"])``
+    accepts it; it travels under ``checkpoint["mi355x"]``."""
+    model = {k: v for k, v in config.model.__dict__.items() if k != "precision"}
+    return {"model": _plain(model), "render": _plain(config.render.__dict__), "data": _plain(config.data.__dict__),
+            "train": _plain(config.train.__dict__)}
+
+
+def noise_dict(noise_config: NoiseConfig) -> dict:
+    return {"rotation_noise_deg": noise_config.rotation_noise_deg, "translation_noise": noise_config.translation_noise,
+            "translation_noise_pct": noise_config.translation_noise_pct, "seed": noise_config.seed}
 
 
 def save_checkpoint(output_dir, iteration: int, model_coarse, model_fine, optimizer: torch.optim.Optimizer,
                     config: NeRFConfig, noise_config=None, metrics: Optional[Dict] = None,
                     is_best: bool = False) -> None:
     """Reference train.py:236-286: same keys (iteration, model_coarse/_fine state_dicts in
-    nn.Linear naming, optimizer state, config as plain dicts), same file names.  The config
-    values are made plain (Path -> str, tuple -> list) so that ``torch.load(...,
-    weights_only=True)`` reads the file back."""
-    from pathlib import Path
-
-    def plain(d):
-        return {k: str(v) if isinstance(v, Path) else list(v) if isinstance(v, tuple) else v for k, v in d.items()}
-
+    nn.Linear naming, optimizer state, config as plain dicts), same file names."""
     output_dir = Path(output_dir)
     output_dir.mkdir(parents=True, exist_ok=True)
     ckpt = {"iteration": iteration, "model_coarse": model_coarse.state_dict(), "optimizer": optimizer.state_dict(),
-            "config": {"model": plain(config.model.__dict__), "render": plain(config.render.__dict__),
-                       "data": plain(config.data.__dict__), "train": plain(config.train.__dict__)}}
+            "config": checkpoint_config(config), "mi355x": {"precision": getattr(config.model, "precision", "fp32")}}
     if model_fine is not None:
         ckpt["model_fine"] = model_fine.state_dict()
     if metrics is not None:
         ckpt["metrics"] = metrics
     if noise_config is not None:
-        ckpt["noise_config"] = {"rotation_noise_deg": noise_config.rotation_noise_deg,
-                                "translation_noise": noise_config.translation_noise,
-                                "translation_noise_pct": noise_config.translation_noise_pct,
-                                "seed": noise_config.seed}
+        ckpt["noise_config"] = noise_dict(noise_config)
     torch.save(ckpt, output_dir / f"checkpoint_{iteration:07d}.pt")
     torch.save(ckpt, output_dir / "checkpoint_latest.pt")
     if is_best:
@@ -142,91 +185,188 @@ def load_checkpoint(checkpoint_path, model_coarse, model_fine, optimizer: Option
     return ckpt.get("iteration", 0)
 
 
-def train(config: NeRFConfig, train_data: BlenderData, val_data: Optional[BlenderData] = None,
-          num_iterations: Optional[int] = None, log=print) -> Dict[str, object]:
-    """Reference train.py:307-577, minus logging/checkpoint I/O: seeds, builds the two
-    networks and the fused Adam + LambdaLR, iterates the epoch sampler, steps."""
+def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
+          train_data: Optional[BlenderData] = None, val_data: Optional[BlenderData] = None,
+          process_group=None, log=print) -> Dict[str, object]:
+    """Reference train.py:307-577.  ``train_data`` / ``val_data`` (optional) replace the
+    on-disk scene; ``process_group`` (or a torchrun environment, see ``main``) makes it
+    data parallel.  Returns the networks, the output directory and the final metrics."""
+    import torch.distributed as dist
+
+    rank, world = 0, 1
+    if process_group is not None:
+        rank, world = dist.get_rank(process_group), dist.get_world_size(process_group)
     set_seed(config.train.seed)
-    coarse, fine = create_nerf(config.model)
-    dev = train_data.images.device
-    coarse, fine = coarse.to(dev), fine.to(dev) if fine is not None else None
-    trainer = Trainer(coarse, fine, config.render, lr=config.train.lr, lr_decay=config.train.lr_decay)
-    sampler = RaySampler(RayDataset(train_data, batch_size=config.data.batch_size), config.data.batch_size,
-                         shuffle=config.data.shuffle)
-    it = iter(sampler)
-    n_iter = num_iterations if num_iterations is not None else config.train.num_iterations
-    t0 = time.time()
-    history = []
-    for step in range(n_iter):
-        try:
-            batch = next(it)
-        except StopIteration:
-            it = iter(sampler)
-            batch = next(it)
-        m = trainer.step(batch["rays_o"], batch["rays_d"], batch["target_rgb"])
-        if (step + 1) % config.train.log_every == 0 or step == n_iter - 1:
-            loss = float(m["loss"])
-            history.append((step, loss))
-            log(f"iter {step + 1}: loss {loss:.5f} lr {trainer.scheduler.get_last_lr()[0]:.4e} "
-                f"({(time.time() - t0) / (step + 1) * 1e3:.2f} ms/it)")
-    result = {"model_coarse": coarse, "model_fine": fine, "history": history}
-    if val_data is not None:
-        result["val"] = evaluate(NeRFRenderer(coarse, fine, config.render), val_data)
+    device = config.train.device
+    if device.startswith("cuda") and not torch.cuda.is_available():
+        raise RuntimeError("noisy_src.train needs a ROCm device (the reference falls back to its CPU path; "
+                           "this framework has no CPU path)")
+    exp_name = config.train.experiment_name
+    if exp_name in ("auto", ""):
+        exp_name = generate_experiment_name(config.data.scene_name, noise_config)
+    output_dir = Path(config.train.output_dir) / exp_name
+    logger = ExperimentLogger(output_dir, exp_name, use_tensorboard=True) if rank == 0 else None
+    if logger is not None:
+        logger.log_config(config)
+
+    if train_data is None:
+        sampler, train_data, val_data = create_data_loaders(config.data, device=device, noise_config=noise_config)
+    else:
+        sampler = RaySampler(RayDataset(train_data, config.data.batch_size, noise_config=noise_config),
+                             config.data.batch_size, shuffle=config.data.shuffle)
+    model_coarse, model_fine = create_nerf(config.model)
+    model_coarse = model_coarse.to(device)
+    model_fine = model_fine.to(device) if config.render.use_hierarchical else None
+    if logger is not None:
+        logger.log_model_info(model_coarse, "model_coarse")
+        if model_fine is not None:
+            logger.log_model_info(model_fine, "model_fine")
+    renderer = NeRFRenderer(model_coarse, model_fine, config.render)
+    trainer = Trainer(model_coarse, model_fine, config.render, lr=config.train.lr, lr_decay=config.train.lr_decay,
+                      process_group=process_group)
+    optimizer = trainer.optimizer
+    lpips_metric = LPIPSMetric(device=device) if rank == 0 else None
+    if lpips_metric is not None and not lpips_metric.available:
+        lpips_metric = None
+    if rank == 0:
+        nc = noise_config
+        (output_dir / "experiment_config.json").write_text(json.dumps({
+            "scene": config.data.scene_name, "experiment_name": exp_name,
+            "noise_config": {"rotation_noise_deg": nc.rotation_noise_deg if nc else 0,
+                             "translation_noise": nc.translation_noise if nc else 0,
+                             "translation_noise_pct": nc.translation_noise_pct if nc else 0,
+                             "seed": nc.seed if nc else None, "has_noise": nc.has_noise if nc else False},
+            "num_iterations": config.train.num_iterations, "batch_size": config.data.batch_size,
+            "img_scale": config.data.img_scale, "timestamp": datetime.now().isoformat(),
+            "data_parallel_ranks": world}, indent=2))
+        log(f"NeRF training: {exp_name} -> {output_dir} ({world} rank(s), {sampler.n_rays:,} rays, "
+            f"{train_data.H}x{train_data.W}, focal {train_data.focal:.2f})")
+
+    B = config.data.batch_size
+    rc = config.render
+    start = time.time()
+    best_psnr = 0.0
+    iteration = 0
+    while iteration < config.train.num_iterations:
+        for batch in sampler:
+            if iteration >= config.train.num_iterations:
+                break
+            n = batch["rays_o"].shape[0]
+            if world > 1 and n % world:
+                continue  # an epoch's ragged tail cannot be split evenly over the ranks: skipped
+            # the global random draws, in the reference's order (jitter, then inverse-CDF
+            # uniforms: rendering.py:161 -> rays.py:204, :255), identical on every rank
+            t_rand = torch.rand(n, rc.num_samples, device=device) if rc.perturb else None
+            u = torch.rand(n, rc.num_samples_fine, device=device) if (rc.use_hierarchical and model_fine) else None
+            sl = rank_slice(n, rank, world) if world > 1 else slice(0, n)
+            t0 = time.time()
+            m = trainer.step(batch["rays_o"][sl], batch["rays_d"][sl], batch["target_rgb"][sl],
+                             t_rand=None if t_rand is None else t_rand[sl], u=None if u is None else u[sl])
+            keys = ["loss", "loss_coarse"] + (["loss_fine"] if "loss_fine" in m else [])
+            vals = mean_over_ranks([m[k] for k in keys], process_group).tolist()
+            batch_time = time.time() - t0
+            vm = dict(zip(keys, vals))
+            last = vm.get("loss_fine", vm["loss_coarse"])
+            psnr = -10.0 * math.log10(last) if last > 0 else float("inf")
+            lr = optimizer.param_groups[0]["lr"]
+            if logger is not None:
+                logger.log_training(TrainingMetrics(iteration=iteration, loss=vm["loss"], loss_coarse=vm["loss_coarse"],
+                                                    loss_fine=vm.get("loss_fine"), psnr=psnr, learning_rate=lr,
+                                                    time_per_iter=batch_time, rays_per_sec=B / batch_time))
+                if iteration % config.train.log_every == 0:
+                    log(f"[{iteration:7d}/{config.train.num_iterations}] loss: {vm['loss']:.5f} | psnr: {psnr:.2f} | "
+                        f"lr: {lr:.2e} | rays/s: {B / batch_time:.0f} | time: {(time.time() - start) / 60:.1f}min")
+                if iteration % config.train.val_every == 0 and iteration > 0:
+                    vmx = evaluate(renderer, val_data, logger, iteration, num_images=5, lpips_metric=lpips_metric)
+                    logger.log_validation(vmx)
+                    is_best = vmx.psnr > best_psnr
+                    best_psnr = max(best_psnr, vmx.psnr)
+                    log(f"  validation @ {iteration}: PSNR {vmx.psnr:.2f} dB, SSIM {vmx.ssim:.4f}"
+                        + (" (best)" if is_best else ""))
+                    save_checkpoint(output_dir, iteration, model_coarse, model_fine, optimizer, config, noise_config,
+                                    metrics={"psnr": vmx.psnr, "ssim": vmx.ssim}, is_best=is_best)
+                elif iteration % config.train.save_every == 0 and iteration > 0:
+                    save_checkpoint(output_dir, iteration, model_coarse, model_fine, optimizer, config, noise_config)
+            iteration += 1
+    result = {"model_coarse": model_coarse, "model_fine": model_fine, "output_dir": output_dir,
+              "best_psnr": best_psnr}
+    if logger is not None:
+        save_checkpoint(output_dir, iteration, model_coarse, model_fine, optimizer, config, noise_config)
+        final = evaluate(renderer, val_data, logger, iteration, num_images=val_data.images.shape[0],
+                         lpips_metric=lpips_metric)
+        logger.log_validation(final)
+        logger.save_summary()
+        logger.close()
+        log(f"final: PSNR {final.psnr:.2f} dB, SSIM {final.ssim:.4f}; {(time.time() - start) / 60:.1f} min; "
+            f"results in {output_dir}")
+        result["val"] = final
+    if process_group is not None:
+        dist.barrier(process_group)
     return result
 
 
-def main(argv=None) -> None:
-    """``python -m noisy_src.train`` — the reference CLI (train.py:580-640), same flags
-    plus ``--precision``; needs the NeRF synthetic scene under ``--data_root``."""
+def build_arg_parser():
+    """Reference train.py:580-657 flags (same names and defaults) plus ``--precision``."""
     import argparse
-    from pathlib import Path
-
-    from .config import DataConfig, ModelConfig, RenderConfig, TrainConfig
-    from .data import load_blender_data
-    from .logger import ExperimentLogger, ValidationMetrics
-
-    ap = argparse.ArgumentParser(description="NeRF training (MI355X HIP path)")
+    ap = argparse.ArgumentParser(description="Train NeRF with optional pose noise (MI355X HIP path)")
     ap.add_argument("--scene", type=str, default="lego")
     ap.add_argument("--data_root", type=str, default=None)
     ap.add_argument("--img_scale", type=float, default=0.5)
-    ap.add_argument("--batch_size", type=int, default=1024)
+    ap.add_argument("--batch_size", type=int, default=1024, help="global batch (rays) over all ranks")
     ap.add_argument("--num_iters", type=int, default=200000)
     ap.add_argument("--lr", type=float, default=5e-4)
     ap.add_argument("--no_hierarchical", action="store_true")
     ap.add_argument("--num_samples", type=int, default=64)
     ap.add_argument("--num_samples_fine", type=int, default=128)
+    ap.add_argument("--rotation_noise", type=float, default=0.0)
+    ap.add_argument("--translation_noise", type=float, default=0.0)
+    ap.add_argument("--translation_noise_pct", type=float, default=0.0)
+    ap.add_argument("--noise_seed", type=int, default=None)
     ap.add_argument("--log_every", type=int, default=100)
     ap.add_argument("--val_every", type=int, default=5000)
+    ap.add_argument("--save_every", type=int, default=10000)
     ap.add_argument("--output_dir", type=str, default="outputs")
     ap.add_argument("--exp_name", type=str, default="auto")
     ap.add_argument("--device", type=str, default="cuda")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16", "fp16"])
-    a = ap.parse_args(argv)
+    ap.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16", "fp16"],
+                    help="MLP operand precision (fp32 = the reference's numerics)")
+    return ap
+
+
+def main(argv=None) -> None:
+    """``python -m noisy_src.train`` (or under ``torchrun`` for data parallelism)."""
+    from .config import DataConfig, ModelConfig, RenderConfig, TrainConfig
+
+    a = build_arg_parser().parse_args(argv)
+    noise_config = None
+    if a.rotation_noise > 0 or a.translation_noise > 0 or a.translation_noise_pct > 0:
+        noise_config = NoiseConfig(rotation_noise_deg=a.rotation_noise, translation_noise=a.translation_noise,
+                                   translation_noise_pct=a.translation_noise_pct, seed=a.noise_seed)
+    pg, rank, world, device = init_distributed(a.device)
     cfg = NeRFConfig(
         model=ModelConfig(precision=a.precision),
-        render=RenderConfig(num_samples=a.num_samples, num_samples_fine=a.num_samples_fine,
-                            use_hierarchical=not a.no_hierarchical),
+        render=RenderConfig(use_hierarchical=not a.no_hierarchical, num_samples=a.num_samples,
+                            num_samples_fine=a.num_samples_fine),
         data=DataConfig(scene_name=a.scene, data_root=Path(a.data_root) if a.data_root else None,
                         img_scale=a.img_scale, batch_size=a.batch_size),
-        train=TrainConfig(lr=a.lr, num_iterations=a.num_iters, log_every=a.log_every, val_every=a.val_every,
-                          output_dir=Path(a.output_dir), experiment_name=a.exp_name, device=a.device, seed=a.seed))
-    root = cfg.data.data_root or Path("data") / "raw"
-    train_data = load_blender_data(root, a.scene, "train", a.img_scale, a.device)
-    val_data = load_blender_data(root, a.scene, "val", a.img_scale, a.device)
-    name = a.exp_name if a.exp_name != "auto" else f"{a.scene}_clean_{time.strftime('%Y%m%d_%H%M%S')}"
-    logger = ExperimentLogger(Path(a.output_dir) / name, name)
-    logger.log_config(cfg)
-    res = train(cfg, train_data, val_data)
-    if "val" in res:
-        v = res["val"]
-        logger.log_validation(ValidationMetrics(iteration=a.num_iters, psnr=v["psnr"], ssim=v["ssim"], mse=v["mse"],
-                                                per_image_psnr=v["per_image_psnr"], per_image_ssim=v["per_image_ssim"]))
-    logger.close()
+        train=TrainConfig(lr=a.lr, num_iterations=a.num_iters, output_dir=Path(a.output_dir),
+                          experiment_name=a.exp_name, device=device, seed=a.seed, log_every=a.log_every,
+                          val_every=a.val_every, save_every=a.save_every))
+    if world > 1 and cfg.train.experiment_name in ("auto", ""):
+        # one shared directory name for all ranks (rank 0's timestamp)
+        import torch.distributed as dist
+        name = [generate_experiment_name(a.scene, noise_config)]
+        dist.broadcast_object_list(name, src=0, group=pg)
+        cfg.train.experiment_name = name[0]
+    train(cfg, noise_config, process_group=pg)
+    if pg is not None:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
-__all__ = ["set_seed", "train_step", "render_image", "evaluate", "save_checkpoint", "load_checkpoint", "train",
-           "lr_lambda_factory", "main"]
+__all__ = ["set_seed", "generate_experiment_name", "train_step", "render_image", "evaluate", "save_checkpoint",
+           "load_checkpoint", "train", "main"]
 
 if __name__ == "__main__":
     main()

@@ -11,11 +11,24 @@ Joint NeRF + camera-pose training step — drop-in for ShawnnnLiu/Robust-NeRF
 * ``train_step_with_poses`` follows train_pose_opt.py:290-411 step for step: poses ->
   rays (one gather kernel) -> render -> MSE coarse+fine -> L2 pose regularisers ->
   backward -> separate clips (coarse 1.0, fine 1.0, poses 0.1) -> the two optimizers.
+* ``train_with_pose_optimization(config, noise_config, init_mode, ...)`` is the
+  reference loop (train_pose_opt.py:613-1054): noisy or clean initial poses, the pose
+  Adam and its LambdaLR only after ``pose_opt_delay``, one CSV row per iteration,
+  validation + pose errors + checkpoint every ``val_every``, checkpoints every
+  ``save_every``, the final evaluation and checkpoint, ``final_poses.pt`` and
+  ``summary.json``.  The step is ``engine.PoseTrainer`` (HIP, no host syncs).  Under
+  ``torchrun`` it is data parallel exactly like ``train.train``: identical global draws
+  on every rank, contiguous slices, network and pose gradients averaged over RCCL.
 """
 
 from __future__ import annotations
 
+import json
+import math
 import random
+import time
+from datetime import datetime
+from pathlib import Path
 from typing import Dict, Optional
 
 import numpy as np
@@ -24,11 +37,14 @@ import torch.nn as nn
 
 from . import ops
 from .config import RenderConfig
-from .data import BlenderData
-from .data_pose_opt import PixelBatch, PixelSampler
-from .metrics import compute_mse, compute_psnr, compute_ssim
+from .config import NeRFConfig
+from .data import BlenderData, load_blender_data
+from .data_pose_opt import PixelBatch, PixelSampler, create_pixel_dataset
+from .engine import PoseTrainer, init_distributed, mean_over_ranks, rank_slice
+from .logger import ExperimentLogger, TrainingMetrics, ValidationMetrics
+from .metrics import LPIPSMetric, compute_mse, compute_psnr, compute_ssim
 from .model import NeRF
-from .noise import compute_pose_error
+from .noise import NoiseConfig, add_noise_to_poses, compute_pose_error
 from .optim import FusedAdam, clip_grad_norm_
 from .rays import get_ray_directions, get_rays
 from .rendering import render_rays
@@ -190,100 +206,225 @@ def render_image_with_pose(model_coarse: NeRF, model_fine: Optional[NeRF], pose:
 @torch.no_grad()
 def evaluate_with_poses(model_coarse: NeRF, model_fine: Optional[NeRF], camera_params: CameraPoseParameters,
                         val_data: BlenderData, val_indices: torch.Tensor, render_config: RenderConfig,
-                        logger=None, iteration: int = 0, num_images: int = 5, lpips_metric=None) -> Dict[str, object]:
+                        logger: Optional[ExperimentLogger] = None, iteration: int = 0, num_images: int = 5,
+                        lpips_metric=None) -> ValidationMetrics:
     """Reference train_pose_opt.py:474-545: renders the first ``num_images`` validation
-    views from their GROUND-TRUTH poses; returns the mean metrics and the per-image lists."""
-    psnr, ssim, mse = [], [], []
-    for idx in val_indices[:min(num_images, len(val_indices))]:
+    views from their GROUND-TRUTH poses (the learnable poses are the training views');
+    PNGs of the first three when a logger is given."""
+    psnr, ssim, mse, lp = [], [], [], []
+    for i, idx in enumerate(val_indices[:min(num_images, len(val_indices))]):
+        idx = int(idx)
         out = render_image_with_pose(model_coarse, model_fine, val_data.poses[idx], val_data.H, val_data.W,
                                      val_data.focal, render_config)
         pred, target = out["rgb"], val_data.images[idx]
         mse.append(compute_mse(pred, target).item())
         psnr.append(compute_psnr(pred, target).item())
         ssim.append(compute_ssim(pred, target).item())
-    return {"iteration": iteration, "psnr": float(np.mean(psnr)), "ssim": float(np.mean(ssim)),
-            "mse": float(np.mean(mse)), "lpips": None, "per_image_psnr": psnr, "per_image_ssim": ssim}
+        if lpips_metric is not None:
+            v = lpips_metric(pred, target)
+            if v is not None:
+                lp.append(v.item())
+        if logger is not None and i < 3:
+            logger.log_images(f"val_{idx}", pred, target, iteration, depth=out["depth"])
+    return ValidationMetrics(iteration=iteration, psnr=float(np.mean(psnr)), ssim=float(np.mean(ssim)),
+                             mse=float(np.mean(mse)), lpips=float(np.mean(lp)) if lp else None,
+                             per_image_psnr=psnr, per_image_ssim=ssim)
 
 
-def train_with_pose_optimization(config, train_data: BlenderData, val_data: Optional[BlenderData] = None,
-                                 init_mode: str = "noisy", noise_config=None, pose_lr: float = 1e-4,
-                                 pose_opt_delay: int = 1000, learn_rotation: bool = True,
-                                 learn_translation: bool = True, rotation_reg_weight: float = 0.01,
-                                 translation_reg_weight: float = 0.001, logger=None, log=print) -> Dict[str, object]:
-    """Reference train_pose_opt.py:613-1054 without the image/checkpoint I/O: seeds, noisy
-    (or clean) initial poses, CameraPoseParameters, both networks, NeRF and pose Adams
-    (fused) with their LambdaLRs (the pose one steps only once poses optimise), the
-    pixel sampler, and train_step_with_poses every iteration."""
-    import time
+def save_checkpoint_with_poses(output_dir, iteration: int, model_coarse, model_fine, camera_params,
+                               optimizer_nerf, optimizer_poses, config: NeRFConfig, noise_config=None,
+                               metrics: Optional[Dict] = None, pose_errors: Optional[Dict] = None,
+                               is_best: bool = False) -> None:
+    """Reference train_pose_opt.py:548-610: the train.py checkpoint plus ``camera_params``,
+    ``optimizer_nerf`` / ``optimizer_poses``, ``initial_poses`` and ``pose_errors``."""
+    from .train import checkpoint_config, noise_dict
+    output_dir = Path(output_dir)
+    output_dir.mkdir(parents=True, exist_ok=True)
+    ckpt = {"iteration": iteration, "model_coarse": model_coarse.state_dict(),
+            "camera_params": camera_params.state_dict(), "optimizer_nerf": optimizer_nerf.state_dict(),
+            "initial_poses": camera_params.initial_poses.cpu(), "config": checkpoint_config(config),
+            "mi355x": {"precision": getattr(config.model, "precision", "fp32")}}
+    if model_fine is not None:
+        ckpt["model_fine"] = model_fine.state_dict()
+    if optimizer_poses is not None:
+        ckpt["optimizer_poses"] = optimizer_poses.state_dict()
+    if metrics is not None:
+        ckpt["metrics"] = metrics
+    if pose_errors is not None:
+        ckpt["pose_errors"] = pose_errors
+    if noise_config is not None:
+        ckpt["noise_config"] = noise_dict(noise_config)
+    torch.save(ckpt, output_dir / f"checkpoint_{iteration:07d}.pt")
+    torch.save(ckpt, output_dir / "checkpoint_latest.pt")
+    if is_best:
+        torch.save(ckpt, output_dir / "checkpoint_best.pt")
 
-    from .data_pose_opt import create_pixel_dataset
-    from .engine import lr_lambda_factory
-    from .logger import TrainingMetrics
-    from .model import create_nerf
-    from .noise import add_noise_to_poses
 
+def generate_experiment_name(scene: str, noise_config: Optional[NoiseConfig], init_mode: str = "noisy") -> str:
+    """Reference train_pose_opt.py:274-287."""
+    ts = datetime.now().strftime("%Y%m%d_%H%M%S")
+    noise_desc = str(noise_config) if noise_config is not None and noise_config.has_noise else "clean"
+    return f"{scene}_poseopt_{init_mode}init_{noise_desc}_{ts}"
+
+
+def train_with_pose_optimization(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None,
+                                 init_mode: str = "noisy", pose_lr: float = 1e-4, pose_opt_delay: int = 1000,
+                                 learn_rotation: bool = True, learn_translation: bool = True,
+                                 rotation_reg_weight: float = 0.01, translation_reg_weight: float = 0.001, *,
+                                 train_data: Optional[BlenderData] = None, val_data: Optional[BlenderData] = None,
+                                 process_group=None, experiment_name: Optional[str] = None,
+                                 log=print) -> Dict[str, object]:
+    """Reference train_pose_opt.py:613-1054 (same arguments, outputs and files).
+    ``train_data`` / ``val_data`` (optional) replace the on-disk scene; ``process_group``
+    makes it data parallel; ``experiment_name`` pins the generated run name (all ranks)."""
+    import torch.distributed as dist
+
+    rank, world = 0, 1
+    if process_group is not None:
+        rank, world = dist.get_rank(process_group), dist.get_world_size(process_group)
     set_seed(config.train.seed)
-    dev = train_data.images.device
-    gt = train_data.poses.clone()
+    device = config.train.device
+    if device.startswith("cuda") and not torch.cuda.is_available():
+        raise RuntimeError("noisy_src.train_pose_opt needs a ROCm device (no CPU path)")
+    exp_name = experiment_name or generate_experiment_name(config.data.scene_name, noise_config, init_mode)
+    output_dir = Path(config.train.output_dir) / exp_name
+    logger = ExperimentLogger(output_dir, exp_name, use_tensorboard=True) if rank == 0 else None
+    if logger is not None:
+        logger.log_config(config)
+    if train_data is None:
+        root = config.data.data_root if config.data.data_root is not None else Path("data") / "raw"
+        train_data = load_blender_data(root, config.data.scene_name, "train", config.data.img_scale, device)
+        val_data = load_blender_data(root, config.data.scene_name, "val", config.data.img_scale, device)
+    gt_train_poses = train_data.poses.clone()
     if init_mode == "noisy" and noise_config is not None and noise_config.has_noise:
-        init, _ = add_noise_to_poses(train_data.poses, noise_config)
-    else:
-        init = gt.clone()
-    cam = CameraPoseParameters(init, learn_rotation, learn_translation).to(dev)
-    mc, mf = create_nerf(config.model)
-    mc = mc.to(dev)
-    mf = mf.to(dev) if config.render.use_hierarchical else None
-    nerf_params = list(mc.parameters()) + (list(mf.parameters()) if mf is not None else [])
-    opt_n = FusedAdam(nerf_params, lr=config.train.lr)
-    opt_p = FusedAdam(cam.parameters(), lr=pose_lr)
-    lam = lr_lambda_factory(config.train.lr_decay)
-    sch_n = torch.optim.lr_scheduler.LambdaLR(opt_n, lam)
-    sch_p = torch.optim.lr_scheduler.LambdaLR(opt_p, lam)
-    _, sampler = create_pixel_dataset(train_data)
-    sampler.batch_size = config.data.batch_size
-    t0 = time.time()
-    for it in range(config.train.num_iterations):
-        batch = sampler.sample_batch()
-        now = it >= pose_opt_delay
-        tb = time.time()
-        m = train_step_with_poses(mc, mf, cam, sampler, opt_n, opt_p if now else None, batch, config.render,
-                                  optimize_poses=now, rotation_reg_weight=rotation_reg_weight,
-                                  translation_reg_weight=translation_reg_weight)
-        sch_n.step()
-        if now:
-            sch_p.step()
-        dt = time.time() - tb
+        initial_poses, _ = add_noise_to_poses(train_data.poses, noise_config)
         if logger is not None:
-            logger.log_training(TrainingMetrics(iteration=it, loss=m["loss"], loss_coarse=m["loss_coarse"],
-                                                loss_fine=m.get("loss_fine"), psnr=m["psnr"],
-                                                learning_rate=opt_n.param_groups[0]["lr"], time_per_iter=dt,
-                                                rays_per_sec=config.data.batch_size / dt))
-        if it % config.train.log_every == 0:
-            log(f"iter {it}: loss {m['loss']:.5f} psnr {m['psnr']:.2f} poses {'on' if now else 'frozen'} "
-                f"({time.time() - t0:.1f} s)")
-    out = {"model_coarse": mc, "model_fine": mf, "camera_params": cam,
-           "pose_errors": cam.compute_pose_errors(gt)}
-    if val_data is not None:
-        out["val"] = evaluate_with_poses(mc, mf, cam, val_data, torch.arange(val_data.images.shape[0]), config.render)
-    return out
+            errs = [compute_pose_error(gt_train_poses[i].cpu(), initial_poses[i].cpu())
+                    for i in range(len(initial_poses))]
+            log(f"initial pose errors: rotation {np.mean([e['rotation_error_deg'] for e in errs]):.3f} deg, "
+                f"translation {np.mean([e['translation_error'] for e in errs]):.4f}")
+    else:
+        initial_poses = gt_train_poses.clone()
+    camera_params = CameraPoseParameters(initial_poses, learn_rotation, learn_translation).to(device)
+    model_coarse, model_fine = create_nerf_for(config, device)
+    if logger is not None:
+        logger.log_model_info(model_coarse, "model_coarse")
+        if model_fine is not None:
+            logger.log_model_info(model_fine, "model_fine")
+    _, pixel_sampler = create_pixel_dataset(train_data)
+    pixel_sampler.batch_size = config.data.batch_size
+    trainer = PoseTrainer(model_coarse, model_fine, camera_params, pixel_sampler, config.render, lr=config.train.lr,
+                          pose_lr=pose_lr, lr_decay=config.train.lr_decay, rotation_reg_weight=rotation_reg_weight,
+                          translation_reg_weight=translation_reg_weight, process_group=process_group)
+    optimizer_nerf, optimizer_poses = trainer.optimizer_nerf, trainer.optimizer_poses
+    lpips_metric = LPIPSMetric(device=device) if rank == 0 else None
+    if lpips_metric is not None and not lpips_metric.available:
+        lpips_metric = None
+    if rank == 0:
+        nc = noise_config
+        (output_dir / "experiment_config.json").write_text(json.dumps({
+            "scene": config.data.scene_name, "experiment_name": exp_name, "init_mode": init_mode,
+            "pose_optimization": {"learn_rotation": learn_rotation, "learn_translation": learn_translation,
+                                  "pose_lr": pose_lr, "pose_opt_delay": pose_opt_delay,
+                                  "rotation_reg_weight": rotation_reg_weight,
+                                  "translation_reg_weight": translation_reg_weight},
+            "noise_config": {"rotation_noise_deg": nc.rotation_noise_deg, "translation_noise": nc.translation_noise,
+                             "translation_noise_pct": nc.translation_noise_pct, "seed": nc.seed,
+                             "has_noise": nc.has_noise} if nc else None,
+            "num_iterations": config.train.num_iterations, "batch_size": config.data.batch_size,
+            "timestamp": datetime.now().isoformat(), "data_parallel_ranks": world}, indent=2))
+        log(f"joint NeRF + pose optimisation: {exp_name} -> {output_dir} ({world} rank(s))")
+
+    B = config.data.batch_size
+    rc = config.render
+    val_idx = torch.arange(val_data.images.shape[0], device=device)
+    start = time.time()
+    best_psnr = 0.0
+    for iteration in range(config.train.num_iterations):
+        batch = pixel_sampler.sample_batch()  # the global batch, identical on every rank
+        now = iteration >= pose_opt_delay
+        t_rand = torch.rand(B, rc.num_samples, device=device) if rc.perturb else None
+        u = torch.rand(B, rc.num_samples_fine, device=device) if (rc.use_hierarchical and model_fine) else None
+        sl = rank_slice(B, rank, world) if world > 1 else slice(0, B)
+        t0 = time.time()
+        m = trainer.step(batch.slice(sl) if world > 1 else batch, optimize_poses=now,
+                         t_rand=None if t_rand is None else t_rand[sl], u=None if u is None else u[sl])
+        keys = ["loss", "loss_coarse"] + (["loss_fine"] if "loss_fine" in m else [])
+        vm = dict(zip(keys, mean_over_ranks([m[k] for k in keys], process_group).tolist()))
+        batch_time = time.time() - t0
+        last = vm.get("loss_fine", vm["loss_coarse"])
+        psnr = -10.0 * math.log10(last) if last > 0 else float("inf")
+        lr = optimizer_nerf.param_groups[0]["lr"]
+        if logger is None:
+            continue
+        logger.log_training(TrainingMetrics(iteration=iteration, loss=vm["loss"], loss_coarse=vm["loss_coarse"],
+                                            loss_fine=vm.get("loss_fine"), psnr=psnr, learning_rate=lr,
+                                            time_per_iter=batch_time, rays_per_sec=B / batch_time))
+        if iteration % config.train.log_every == 0:
+            log(f"[{iteration:7d}/{config.train.num_iterations}] loss: {vm['loss']:.5f} | psnr: {psnr:.2f} | "
+                f"lr: {lr:.2e} | poses: {'optimizing' if now else 'frozen'} | "
+                f"time: {(time.time() - start) / 60:.1f}min")
+        if iteration % config.train.val_every == 0 and iteration > 0:
+            pe = camera_params.compute_pose_errors(gt_train_poses)
+            vmx = evaluate_with_poses(model_coarse, model_fine, camera_params, val_data, val_idx, rc, logger,
+                                      iteration, num_images=5, lpips_metric=lpips_metric)
+            logger.log_validation(vmx)
+            is_best = vmx.psnr > best_psnr
+            best_psnr = max(best_psnr, vmx.psnr)
+            log(f"  validation @ {iteration}: PSNR {vmx.psnr:.2f} dB; pose error rot "
+                f"{pe['rotation_error_mean']:.3f} deg, trans {pe['translation_error_mean']:.4f}")
+            save_checkpoint_with_poses(output_dir, iteration, model_coarse, model_fine, camera_params,
+                                       optimizer_nerf, optimizer_poses, config, noise_config,
+                                       metrics={"psnr": vmx.psnr, "ssim": vmx.ssim}, pose_errors=pe,
+                                       is_best=is_best)
+        elif iteration % config.train.save_every == 0 and iteration > 0:
+            pe = camera_params.compute_pose_errors(gt_train_poses)
+            save_checkpoint_with_poses(output_dir, iteration, model_coarse, model_fine, camera_params,
+                                       optimizer_nerf, optimizer_poses, config, noise_config, pose_errors=pe)
+    result = {"model_coarse": model_coarse, "model_fine": model_fine, "camera_params": camera_params,
+              "output_dir": output_dir, "pose_errors": camera_params.compute_pose_errors(gt_train_poses)}
+    if logger is not None:
+        final_pe = result["pose_errors"]
+        final = evaluate_with_poses(model_coarse, model_fine, camera_params, val_data, val_idx, rc, logger,
+                                    config.train.num_iterations, num_images=val_data.images.shape[0],
+                                    lpips_metric=lpips_metric)
+        # (the reference does not write the final evaluation to val_metrics.csv, :1002-1019)
+        save_checkpoint_with_poses(output_dir, config.train.num_iterations, model_coarse, model_fine, camera_params,
+                                   optimizer_nerf, optimizer_poses, config, noise_config,
+                                   metrics={"psnr": final.psnr, "ssim": final.ssim}, pose_errors=final_pe)
+        with torch.no_grad():
+            final_poses = camera_params.get_all_poses()
+        torch.save({"initial_poses": camera_params.initial_poses.cpu(), "optimized_poses": final_poses.cpu(),
+                    "ground_truth_poses": gt_train_poses.cpu(), "pose_errors": final_pe},
+                   output_dir / "final_poses.pt")
+        logger.save_summary()
+        logger.close()
+        log(f"final: PSNR {final.psnr:.2f} dB; pose error rot {final_pe['rotation_error_mean']:.3f} deg, "
+            f"trans {final_pe['translation_error_mean']:.4f}; results in {output_dir}")
+        result["val"] = final
+    if process_group is not None:
+        dist.barrier(process_group)
+    return result
 
 
-def main(argv=None) -> None:
-    """``python -m noisy_src.train_pose_opt`` — the reference CLI (train_pose_opt.py:1057-1190),
-    same flags plus ``--precision``; needs the NeRF synthetic scene under ``--data_root``."""
+def create_nerf_for(config: NeRFConfig, device):
+    """create_nerf + .to(device); no fine network without hierarchical sampling
+    (train_pose_opt.py:772-777)."""
+    from .model import create_nerf
+    mc, mf = create_nerf(config.model)
+    mc = mc.to(device)
+    mf = mf.to(device) if config.render.use_hierarchical else None
+    return mc, mf
+
+
+def build_arg_parser():
+    """Reference train_pose_opt.py:1057-1142 flags (same names and defaults) plus ``--precision``."""
     import argparse
-    from pathlib import Path
-
-    from .config import DataConfig, ModelConfig, NeRFConfig, TrainConfig
-    from .data import load_blender_data
-    from .logger import ExperimentLogger
-    from .noise import NoiseConfig
-
     ap = argparse.ArgumentParser(description="Joint NeRF + camera pose optimisation (MI355X HIP path)")
     ap.add_argument("--scene", type=str, default="lego")
     ap.add_argument("--data_root", type=str, default=None)
     ap.add_argument("--img_scale", type=float, default=0.5)
-    ap.add_argument("--batch_size", type=int, default=1024)
+    ap.add_argument("--batch_size", type=int, default=1024, help="global batch (pixels) over all ranks")
     ap.add_argument("--num_iters", type=int, default=50000)
     ap.add_argument("--lr", type=float, default=5e-4)
     ap.add_argument("--init_mode", type=str, default="noisy", choices=["noisy", "clean"])
@@ -301,33 +442,49 @@ def main(argv=None) -> None:
     ap.add_argument("--num_samples", type=int, default=64)
     ap.add_argument("--num_samples_fine", type=int, default=128)
     ap.add_argument("--log_every", type=int, default=100)
+    ap.add_argument("--val_every", type=int, default=2500)
+    ap.add_argument("--save_every", type=int, default=10000)
     ap.add_argument("--output_dir", type=str, default="outputs")
     ap.add_argument("--device", type=str, default="cuda")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16", "fp16"])
-    a = ap.parse_args(argv)
+    ap.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16", "fp16"],
+                    help="MLP operand precision (fp32 = the reference's numerics)")
+    return ap
+
+
+def main(argv=None) -> None:
+    """``python -m noisy_src.train_pose_opt`` (or under ``torchrun`` for data parallelism)."""
+    from .config import DataConfig, ModelConfig, TrainConfig
+
+    a = build_arg_parser().parse_args(argv)
+    noise_config = None
+    if a.rotation_noise > 0 or a.translation_noise > 0 or a.translation_noise_pct > 0:
+        noise_config = NoiseConfig(rotation_noise_deg=a.rotation_noise, translation_noise=a.translation_noise,
+                                   translation_noise_pct=a.translation_noise_pct, seed=a.noise_seed)
+    pg, rank, world, device = init_distributed(a.device)
     cfg = NeRFConfig(
         model=ModelConfig(precision=a.precision),
-        render=RenderConfig(num_samples=a.num_samples, num_samples_fine=a.num_samples_fine,
-                            use_hierarchical=not a.no_hierarchical),
+        render=RenderConfig(use_hierarchical=not a.no_hierarchical, num_samples=a.num_samples,
+                            num_samples_fine=a.num_samples_fine),
         data=DataConfig(scene_name=a.scene, data_root=Path(a.data_root) if a.data_root else None,
                         img_scale=a.img_scale, batch_size=a.batch_size),
-        train=TrainConfig(lr=a.lr, num_iterations=a.num_iters, log_every=a.log_every,
-                          output_dir=Path(a.output_dir), device=a.device, seed=a.seed))
-    noise = NoiseConfig(rotation_noise_deg=a.rotation_noise, translation_noise=a.translation_noise,
-                        translation_noise_pct=a.translation_noise_pct, seed=a.noise_seed)
-    root = cfg.data.data_root or Path("data") / "raw"
-    train_data = load_blender_data(root, a.scene, "train", a.img_scale, a.device)
-    val_data = load_blender_data(root, a.scene, "val", a.img_scale, a.device)
-    import time
-    name = f"{a.scene}_poseopt_{a.init_mode}init_{noise}_{time.strftime('%Y%m%d_%H%M%S')}"  # (:274-287)
-    logger = ExperimentLogger(Path(a.output_dir) / name, name)
-    logger.log_config(cfg)
-    train_with_pose_optimization(cfg, train_data, val_data, a.init_mode, noise, a.pose_lr, a.pose_opt_delay,
+        train=TrainConfig(lr=a.lr, num_iterations=a.num_iters, output_dir=Path(a.output_dir), device=device,
+                          seed=a.seed, log_every=a.log_every, val_every=a.val_every, save_every=a.save_every))
+    name = [generate_experiment_name(a.scene, noise_config, a.init_mode)]
+    if pg is not None:
+        import torch.distributed as dist
+        dist.broadcast_object_list(name, src=0, group=pg)
+    train_with_pose_optimization(cfg, noise_config, a.init_mode, a.pose_lr, a.pose_opt_delay,
                                  not a.no_learn_rotation, not a.no_learn_translation, a.rotation_reg_weight,
-                                 a.translation_reg_weight, logger=logger)
-    logger.close()
+                                 a.translation_reg_weight, process_group=pg, experiment_name=name[0])
+    if pg is not None:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
+
+__all__ = ["set_seed", "CameraPoseParameters", "train_step_with_poses", "render_image_with_pose",
+           "evaluate_with_poses", "save_checkpoint_with_poses", "generate_experiment_name",
+           "train_with_pose_optimization", "main"]
 
 if __name__ == "__main__":
     main()

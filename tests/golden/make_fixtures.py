@@ -83,8 +83,63 @@ def extract_logs() -> dict:
     return out
 
 
+def _pickle_strings(pkl: bytes) -> list:
+    """Every BINUNICODE string of a pickle stream, in order (opcode 'X' + 4-byte length),
+    read as bytes -- the key names of a saved dict, without unpickling."""
+    out, i = [], 0
+    while True:
+        i = pkl.find(b"X", i)
+        if i < 0 or i + 5 > len(pkl):
+            return out
+        n = struct.unpack("<I", pkl[i + 1:i + 5])[0]
+        if 0 < n < 64 and i + 5 + n <= len(pkl):
+            try:
+                t = pkl[i + 5:i + 5 + n].decode("ascii")
+                if t.isidentifier():
+                    out.append(t)
+                    i += 5 + n
+                    continue
+            except UnicodeDecodeError:
+                pass
+        i += 1
+
+
+def extract_layout() -> dict:
+    """The reference's output-folder contract per run kind (train.py vs train_pose_opt.py):
+    top-level files, logs/ files, CSV headers, JSON key sets, image-name patterns and the
+    key names inside final_poses.pt."""
+    out = {}
+    for run_dir in sorted(REF.iterdir()):
+        kind = "pose_opt" if "poseopt" in run_dir.name else "train"
+        rec = out.setdefault(kind, {"runs": [], "top_files": None, "log_files": set(), "csv_headers": {},
+                                    "summary_keys": None, "experiment_config_keys": None, "config_keys": None,
+                                    "image_patterns": set(), "final_poses_keys": None})
+        rec["runs"].append(run_dir.name)
+        top = sorted(f.name for f in run_dir.iterdir() if f.name != "results.txt")
+        rec["top_files"] = top
+        for f in sorted((run_dir / "logs").glob("*.csv")):
+            rec["log_files"].add(f.name)
+            rec["csv_headers"][f.name] = f.read_text().splitlines()[0]
+        for name, key in (("summary.json", "summary_keys"), ("experiment_config.json", "experiment_config_keys"),
+                          ("config.json", "config_keys")):
+            rec[key] = sorted(json.loads((run_dir / name).read_text()).keys())
+        for img in (run_dir / "images").glob("*.png"):
+            rec["image_patterns"].add(re.sub(r"\d{7}", "{it:07d}", re.sub(r"^val_\d+", "val_{i}", img.name)))
+        fp = run_dir / "final_poses.pt"
+        if fp.exists():
+            z = zipfile.ZipFile(fp)
+            prefix = z.namelist()[0].split("/")[0]
+            names = _pickle_strings(z.read(f"{prefix}/data.pkl"))
+            rec["final_poses_keys"] = [k for k in ("initial_poses", "optimized_poses", "ground_truth_poses",
+                                                   "pose_errors") if k in names]
+    for rec in out.values():
+        rec["log_files"] = sorted(rec["log_files"])
+        rec["image_patterns"] = sorted(rec["image_patterns"])
+    return out
+
+
 def main():
-    artifacts = {"final_poses": extract_final_poses(), "runs": extract_logs()}
+    artifacts = {"final_poses": extract_final_poses(), "runs": extract_logs(), "layout": extract_layout()}
     (OUT / "reference_artifacts.json").write_text(json.dumps(artifacts, indent=1, sort_keys=True))
     print("wrote", OUT)
 

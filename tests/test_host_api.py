@@ -2,6 +2,7 @@
 (data.py), pose noise (noise.py), metrics (metrics.py) and the CSV schema of the
 logger (logger.py), each against the reference behaviour it restates."""
 import json
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -107,17 +108,20 @@ def test_ssim_identity_and_numpy_restatement():
 
 
 def test_logger_csv_schema(tmp_path):
-    """The train/val CSV headers of the reference's outputs/*/logs (logger.py:111-156)."""
+    """The train/val CSV headers and locations of the reference's outputs/*/logs
+    (logger.py:111-156) and its summary.json keys (logger.py:338-363)."""
     from noisy_src.logger import ExperimentLogger, TrainingMetrics, ValidationMetrics
     lg = ExperimentLogger(tmp_path, "exp")
     lg.log_training(TrainingMetrics(iteration=0, loss=0.3, loss_coarse=0.1, loss_fine=0.2, psnr=6.8,
                                     learning_rate=4.99995e-4, time_per_iter=0.3, rays_per_sec=3319.5))
     lg.log_validation(ValidationMetrics(iteration=5000, psnr=24.4, ssim=0.85, mse=0.0037, per_image_psnr=[1.0]))
+    lg.save_summary()
     lg.close()
-    assert (tmp_path / "train_metrics.csv").read_text().splitlines()[0] == \
-        "iteration,loss,loss_coarse,loss_fine,psnr,learning_rate,time_per_iter,rays_per_sec"
-    assert (tmp_path / "val_metrics.csv").read_text().splitlines()[0] == "iteration,psnr,ssim,mse"
-    assert json.loads((tmp_path / "summary.json").read_text())["best_psnr"] == 24.4
+    lay = json.loads((Path(__file__).parent / "golden" / "reference_artifacts.json").read_text())["layout"]["train"]
+    for f in ("train_metrics.csv", "val_metrics.csv"):
+        assert (tmp_path / "logs" / f).read_text().splitlines()[0] == lay["csv_headers"][f]
+    summ = json.loads((tmp_path / "summary.json").read_text())
+    assert summ["best_val_psnr"] == 24.4 and summ["final_val_ssim"] == 0.85 and summ["total_iterations"] == 1
 
 
 def test_package_exports_reference_names():

@@ -9,6 +9,7 @@ under test).  The GPU test renders through the HIP path."""
 import json
 import os
 import socket
+from dataclasses import dataclass
 
 import pytest
 import torch
@@ -39,7 +40,8 @@ def test_checkpoint_round_trip(tmp_path):
     for name in ("checkpoint_0001234.pt", "checkpoint_latest.pt", "checkpoint_best.pt"):
         assert (tmp_path / name).exists()
     ck = torch.load(tmp_path / "checkpoint_latest.pt", weights_only=True)
-    assert set(ck) == {"iteration", "model_coarse", "model_fine", "optimizer", "config", "metrics", "noise_config"}
+    assert set(ck) == {"iteration", "model_coarse", "model_fine", "optimizer", "config", "metrics", "noise_config",
+                       "mi355x"}
     assert list(ck["model_coarse"]) == list(mc.state_dict())  # nn.Linear naming of the reference
     renderer, c, it = inference.load_checkpoint(tmp_path / "checkpoint_latest.pt", device="cpu")
     assert it == 1234 and c["model"]["hidden_dim"] == 256 and c["render"]["num_samples_fine"] == 128
@@ -53,6 +55,56 @@ def test_checkpoint_round_trip(tmp_path):
     s2, s1 = mc2.state_dict(), mc.state_dict()
     assert all(torch.equal(s2[k], s1[k]) for k in s1)
     assert opt2.state_dict()["param_groups"][0]["lr"] == 5e-4
+
+
+@dataclass
+class _RefModelConfig:
+    """The reference's ModelConfig fields only (noisy_src/config.py:10-24)."""
+
+    pos_freqs: int = 10
+    dir_freqs: int = 4
+    hidden_dim: int = 256
+    num_hidden_layers: int = 8
+    skips: tuple = (4,)
+    use_view_dirs: bool = True
+
+
+def test_checkpoint_readable_by_reference_loaders(tmp_path):
+    """A checkpoint written from FusedAdam loads where the reference loads it: its
+    ``ModelConfig(**cfg["model"])`` (inference.py:53) and a plain ``torch.optim.Adam``
+    whose ``step()`` reads every Adam param-group key."""
+    from noisy_src.model import create_nerf
+    from noisy_src.optim import FusedAdam
+    from noisy_src.train import save_checkpoint
+    cfg = NeRFConfig()
+    cfg.model.precision = "bf16"
+    torch.manual_seed(0)
+    mc, mf = create_nerf(cfg.model)
+    fused = FusedAdam(list(mc.parameters()) + list(mf.parameters()), lr=5e-4)
+    save_checkpoint(tmp_path, 7, mc, mf, fused, cfg)
+    ck = torch.load(tmp_path / "checkpoint_latest.pt", weights_only=True)
+    _RefModelConfig(**ck["config"]["model"])  # no unexpected keyword
+    assert ck["mi355x"]["precision"] == "bf16"
+    renderer, _, _ = inference.load_checkpoint(tmp_path / "checkpoint_latest.pt", device="cpu")
+    assert renderer.model_coarse.config.precision == "bf16"
+    torch.manual_seed(1)
+    a, b = create_nerf(cfg.model)
+    params = list(a.parameters()) + list(b.parameters())
+    adam = torch.optim.Adam(params, lr=1.0)
+    adam.load_state_dict(ck["optimizer"])
+    assert adam.param_groups[0]["lr"] == 5e-4
+    for p in params:
+        p.grad = torch.ones_like(p)
+    adam.step()  # KeyError on a missing param-group key would surface here
+
+
+def test_fused_adam_rejects_unsupported_options():
+    from noisy_src.optim import FusedAdam
+    p = [torch.nn.Parameter(torch.zeros(4))]
+    with pytest.raises(ValueError):
+        FusedAdam(p, weight_decay=0.1)
+    with pytest.raises(ValueError):
+        FusedAdam(p, amsgrad=True)
 
 
 def _fake_render(renderer, pose, H, W, focal, chunk_size=4096):

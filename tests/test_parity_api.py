@@ -188,7 +188,7 @@ def test_render_image_matches_render_rays():
     assert (got["acc"].reshape(-1).cpu() - want["acc_fine"]).abs().max() < 1e-4
     val = synthetic_blender_data(_gt_poses()[:2], H=12, W=10, device=DEV)
     m = evaluate(NeRFRenderer(mc, mf, rc), val, num_images=2)
-    assert np.isfinite(m["psnr"]) and 0 < m["ssim"] <= 1
+    assert np.isfinite(m.psnr) and 0 < m.ssim <= 1 and len(m.per_image_psnr) == 2
 
 
 def test_pose_trainer_matches_train_step_with_poses():
@@ -228,7 +228,7 @@ def test_pose_trainer_matches_train_step_with_poses():
         assert abs(float(m["loss"]) - got["loss"]) < 1e-6, step
     assert torch.equal(mc_a.flat_params(), mc_b.flat_params())
     assert torch.equal(mf_a.flat_params(), mf_b.flat_params())
-    # the pose gradient is scattered with float atomics (order varies run to run): ulps
-    assert (cam_a.translation_deltas.detach() - cam_b.translation_deltas.detach()).abs().max() < 2e-6
+    # the pose gradient is a fixed-order segmented reduction: bit-identical
+    assert torch.equal(cam_a.translation_deltas.detach(), cam_b.translation_deltas.detach())
     assert cam_b.translation_deltas.detach().abs().max() > 1e-6
     assert opt_p.param_groups[0]["lr"] == trainer.optimizer_poses.param_groups[0]["lr"]
