@@ -11,9 +11,11 @@ per step (weak scaling), bf16 MFMA MLP with fp32 master weights.  The scene
 content is synthetic (random targets): the lego dataset is not available here.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--precision bf16|fp16|fp32]
-                    [--num-samples 64 --num-samples-fine 128]
+                    [--num-samples 64 --num-samples-fine 128] [--global-batch G] [--pose-opt]
 
-(BASELINE cfg #5 is --precision fp16 --num-samples 128 --num-samples-fine 256.)
+(BASELINE cfg #5 is --precision fp16 --num-samples 128 --num-samples-fine 256; cfg #3 is
+--pose-opt; cfg #4's strong-scaling leg is --global-batch 4096 under torchrun, where every
+rank draws the same global batches and trains on its contiguous slice.)
 
 For N > 1 the driver runs it under torch.distributed.run (one rank per GPU).
 Rank 0 prints ONE JSON line.
@@ -80,12 +82,13 @@ def roofline_of(entry: str, M: int, ms: float, prec: str, n_params: int):
     return "hbm", nbytes / (ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s", f"{n_params} fp32 grads"
 
 
-def lego_rays(n_rays: int, seed: int, device):
-    """Rays of the lego 800x800 training cameras (focal from camera_angle_x, data.py:147-150)."""
+def lego_rays(n_rays: int, seed: int, device, size: int = 800):
+    """Rays of the lego training cameras at size x size (focal from camera_angle_x,
+    data.py:147-150)."""
     g = torch.Generator().manual_seed(seed)
     fix = sorted((ROOT / "tests" / "golden").glob("final_poses_*.npz"))[0]
     poses = torch.from_numpy(np.load(fix)["ground_truth_poses"])
-    H = W = 800
+    H = W = size
     focal = 0.5 * W / math.tan(0.5 * 0.6911112070083618)
     img = torch.randint(0, poses.shape[0], (n_rays,), generator=g)
     i = torch.randint(0, W, (n_rays,), generator=g).float()
@@ -116,41 +119,109 @@ def pose_opt_setup(H: int, W: int, device):
 
 
 def psnr_record():
-    """Summary of profiles/r01_psnr_parity.json (tests/psnr_parity.py, run on the GPU box):
-    test PSNR at equal iterations of this engine vs the oracle, not measured in this run."""
-    f = ROOT / "profiles" / "r01_psnr_parity.json"
-    if not f.exists():
+    """The latest committed test-PSNR record (profiles/r*_psnr_parity.json, written by
+    tests/psnr_parity.py on the GPU box): RECORDED, not measured in this run."""
+    recs = sorted((ROOT / "profiles").glob("r*_psnr_parity.json"))
+    if not recs:
         return None
+    f = recs[-1]
     rec = json.loads(f.read_text())
     if "summary" not in rec:
         return None
-    return {"source": "profiles/r01_psnr_parity.json (recorded, tests/psnr_parity.py)",
-            "scene": "analytic 3-sphere scene, lego train cameras, 10 test views",
+    return {"recorded": True, "source": f"profiles/{f.name} (tests/psnr_parity.py)",
+            "commit": rec.get("commit"), "scene": rec.get("scene", "analytic 3-sphere scene, lego train cameras"),
             "iters": rec["iters"], "seeds": rec["seeds"],
             "mean_db": {k: round(v["mean"], 3) for k, v in rec["summary"].items()},
             "delta_db_vs_ref": {k: v["delta_mean_db"] for k, v in rec["delta_vs_ref"].items()},
             "se_of_delta_db": {k: v["se_of_delta_db"] for k, v in rec["delta_vs_ref"].items()}}
 
 
-def cpu_baseline(n_rays: int, steps: int):
-    """The oracle (torch CPU restatement of the reference) training step, 64c+128f."""
-    from types import SimpleNamespace
+def _cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
+
+def _cpu_leg(rc, n_rays: int, steps: int, warmup: int):
+    """Per-step wall times of the oracle's reference train step (train.py:68-119 + the
+    scheduler step; the rays/s interval of train.py:455-465) on the host CPU."""
     from oracle import refimpl as ref
-    torch.manual_seed(0)
-    rc = SimpleNamespace(near=2.0, far=6.0, num_samples=64, num_samples_fine=128, use_hierarchical=True,
-                         perturb=True, raw_noise_std=0.0, white_background=True)
+    torch.manual_seed(42)
     mc, mf = ref.create_nerf()
+    if not rc.use_hierarchical:
+        mf = None
     state = ref.TrainState(mc, mf)
-    o, d, t = lego_rays(n_rays, 123, "cpu")
-    ref.train_step(mc, mf, state, o, d, t, rc)  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    o, d, t = lego_rays(n_rays, 123, "cpu", size=400)  # cfg #1: img_scale 0.5
+    times = []
+    for k in range(warmup + steps):
+        t0 = time.perf_counter()
         ref.train_step(mc, mf, state, o, d, t, rc)
-    dt = time.perf_counter() - t0
-    return {"value": n_rays * steps / dt, "unit": "rays/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle/refimpl.py train_step (fp32, torch CPU), {n_rays} rays x {steps} steps, "
-                      f"64c+128f, lego 800x800 camera rays; {dt:.1f} s"}
+        if k >= warmup:
+            times.append(time.perf_counter() - t0)
+    times.sort()
+    q = lambda f: times[min(len(times) - 1, int(f * len(times)))]  # noqa: E731
+    return {"rays_per_s_median": n_rays / q(0.5), "rays_per_s_p10": n_rays / q(0.9), "rays_per_s_p90": n_rays / q(0.1),
+            "step_s_median": q(0.5), "steps": steps, "warmup": warmup, "seconds": sum(times)}
+
+
+def cpu_baseline(steps: int = 50, warmup: int = 5, context_steps: int = 3):
+    """the reference CPU path -- the oracle (op-for-op torch restatement of
+    the reference; the reference itself is not shipped to the GPU box) -- on BASELINE
+    cfg #1 (lego 400x400 cameras, coarse-only 64 samples, 256-ray batch, fp32), 5 warm-up
+    + 50 timed steps, median/p10/p90, all host cores the process may use; plus a few
+    steps of 64c+128f at 256 rays for context."""
+    from types import SimpleNamespace
+    affinity = len(os.sched_getaffinity(0))
+    # the GPU box grants a CPU share (OMP_NUM_THREADS) smaller than the machine's affinity mask
+    threads = min(affinity, int(os.environ.get("OMP_NUM_THREADS", affinity)))
+    torch.set_num_threads(threads)
+    rc1 = SimpleNamespace(near=2.0, far=6.0, num_samples=64, num_samples_fine=128, use_hierarchical=False,
+                          perturb=True, raw_noise_std=0.0, white_background=True)
+    c1 = _cpu_leg(rc1, 256, steps, warmup)
+    rc2 = SimpleNamespace(**{**rc1.__dict__, "use_hierarchical": True})
+    c2 = _cpu_leg(rc2, 256, context_steps, 1)
+    return {"value": round(c1["rays_per_s_median"], 2), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"BASELINE cfg #1: oracle/refimpl.py train_step (fp32 torch CPU), lego 400x400 camera rays, "
+                      f"coarse-only 64 samples, 256 rays, {warmup} warm-up + {steps} timed steps "
+                      f"({c1['seconds']:.1f} s); value = median",
+            "p10_p50_p90_rays_per_s": [round(c1["rays_per_s_p10"], 2), round(c1["rays_per_s_median"], 2),
+                                       round(c1["rays_per_s_p90"], 2)],
+            "cpu_model": _cpu_model(), "affinity_cpus": affinity, "threads": threads,
+            "context_64c128f_256rays": {"rays_per_s_median": round(c2["rays_per_s_median"], 2),
+                                        "steps": context_steps, "seconds": round(c2["seconds"], 1)}}
+
+
+def batch_assembly_ms(device, B: int, steps: int = 50):
+    """the per-step cost of the reference's batch assembly, timed on its own
+    (the reference's rays/s interval excludes it, train.py:455): RaySampler over the
+    device ray table of 100 lego 800x800 training views (64 M rays, 2.3 GB resident),
+    one nr_gather_rays launch per batch, and PixelSampler.sample_batch (pose-opt)."""
+    from noisy_src.data import RayDataset, RaySampler, synthetic_blender_data
+    from noisy_src.data_pose_opt import create_pixel_dataset
+    fix = sorted((ROOT / "tests" / "golden").glob("final_poses_*.npz"))[0]
+    data = synthetic_blender_data(torch.from_numpy(np.load(fix)["ground_truth_poses"]), 800, 800, device=device)
+    sampler = RaySampler(RayDataset(data, B), B, shuffle=True)
+    it = iter(sampler)
+    _, psampler = create_pixel_dataset(data)
+    psampler.batch_size = B
+    out = {}
+    for name, fn in (("ray_sampler", lambda: next(it)), ("pixel_sampler", psampler.sample_batch)):
+        fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(steps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        out[name] = round(s.elapsed_time(e) / steps, 4)
+    del sampler, it, psampler, data
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -162,8 +233,10 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--num-samples", type=int, default=64)
     ap.add_argument("--num-samples-fine", type=int, default=128)
-    ap.add_argument("--cpu-rays", type=int, default=1024)
-    ap.add_argument("--cpu-steps", type=int, default=4)
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling (BASELINE cfg #4): one shared global batch of this many rays, "
+                         "sliced over the ranks (default 0: weak scaling, --batch rays per GPU)")
+    ap.add_argument("--cpu-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pose-opt", action="store_true",
                     help="BASELINE cfg #3: joint pose optimisation step (train_pose_opt, poses optimising)")
@@ -189,18 +262,33 @@ def main():
     mc, mf = create_nerf(ModelConfig(precision=args.precision))
     mc, mf = mc.to(dev), mf.to(dev)
     rcfg = RenderConfig(num_samples=args.num_samples, num_samples_fine=args.num_samples_fine)
-    B = args.batch
+    strong = args.global_batch > 0
+    if strong:
+        if args.global_batch % world:
+            raise SystemExit(f"--global-batch {args.global_batch} is not divisible by {world} ranks")
+        B = args.global_batch // world
+        sl = slice(rank * B, (rank + 1) * B)
+    else:
+        B = args.batch
     if args.pose_opt:
         # rays come from (image, pixel) and the learnable poses INSIDE the step; the
         # pixel draws (sampler.sample_batch) stay outside it, as batch sampling does below
         cam, sampler = pose_opt_setup(800, 800, dev)
         sampler.batch_size = B
         trainer = PoseTrainer(mc, mf, cam, sampler, rcfg, process_group=pg)
-        gen = torch.Generator(device=dev).manual_seed(1000 * rank)
-        pool = [sampler.sample_batch(generator=gen) for _ in range(4)]
+        if strong:  # every rank draws the same global batches and takes its slice
+            sampler.batch_size = args.global_batch
+            gen = torch.Generator(device=dev).manual_seed(1000)
+            pool = [sampler.sample_batch(generator=gen).slice(sl) for _ in range(4)]
+        else:
+            gen = torch.Generator(device=dev).manual_seed(1000 * rank)
+            pool = [sampler.sample_batch(generator=gen) for _ in range(4)]
     else:
         trainer = Trainer(mc, mf, rcfg, process_group=pg)
-        pool = [lego_rays(B, 1000 * rank + k, dev) for k in range(4)]
+        if strong:
+            pool = [tuple(x[sl] for x in lego_rays(args.global_batch, 1000 + k, dev)) for k in range(4)]
+        else:
+            pool = [lego_rays(B, 1000 * rank + k, dev) for k in range(4)]
     torch.manual_seed(1234 + rank)
 
     def step(k):
@@ -255,14 +343,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * dt / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": args.precision,
         "data": "synthetic (lego 800x800 camera rays from the reference's GT poses; random targets)",
         "config": {
             "workload": (f"lego 800x800 joint pose-opt (5 deg rot + 5% trans noisy init, SE(3) pose grads) "
                          if args.pose_opt else "lego 800x800 ")
-                        + f"hierarchical {rcfg.num_samples}c+{rcfg.num_samples_fine}f training step, {B} rays per GPU",
+                        + f"hierarchical {rcfg.num_samples}c+{rcfg.num_samples_fine}f training step, "
+                        + (f"global batch {args.global_batch} rays sliced over {world} GPU(s)" if strong
+                           else f"{B} rays per GPU"),
             "global_batch": world * B,
             "num_samples": rcfg.num_samples,
             "num_samples_fine": rcfg.num_samples_fine,
@@ -290,8 +380,10 @@ def main():
         # metric is the recorded equal-iteration comparison on the analytic scene
         "psnr": psnr_record(),
     }
+    if rank == 0 and world == 1:
+        out["batch_assembly_ms_per_step"] = batch_assembly_ms(dev, B)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.pose_opt:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_rays, args.cpu_steps)
+        out["cpu_baseline"] = cpu_baseline(steps=args.cpu_steps)
     if rank == 0:
         print(json.dumps(out))
     if pg is not None:

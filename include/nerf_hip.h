@@ -54,6 +54,16 @@ int nr_ray_directions(int H, int W, float focal, float cx, float cy,
  * dirs (N,3), c2w (4,4) -> rays_o (N,3) = t, rays_d (N,3) = normalize(R d). */
 int nr_get_rays(const float* dirs, const float* c2w, int64_t N,
                 float* rays_o, float* rays_d, nr_stream_t stream);
+/* Backward of get_rays (the reference's is differentiable in c2w and dirs):
+ * g_c2w (4,4) ACCUMULATED (caller zeroes), rows 0..2 / cols 0..3 (R and t);
+ * g_dirs (N,3) OVERWRITTEN, nullable; g_rays_o / g_rays_d nullable (not both;
+ * g_dirs needs g_rays_d).  Fixed-order reduction over the N rays through
+ * nr_get_rays_bwd_workspace_bytes() of scratch.                             */
+int64_t nr_get_rays_bwd_workspace_bytes(void);
+int nr_get_rays_bwd(const float* dirs, const float* c2w, int64_t N,
+                    const float* g_rays_o, const float* g_rays_d,
+                    float* g_dirs, float* g_c2w, void* workspace,
+                    nr_stream_t stream);
 
 /* ---- A3: PixelDataset.get_rays_from_pixels  (noisy_src/data_pose_opt.py:83-148,
  *          PixelSampler.get_rays_for_batch :200-223) ---------------------
@@ -97,6 +107,13 @@ int nr_se3_poses_bwd(const float* init_poses, const float* rot_deltas,
                      const float* g_poses,
                      int fixed_small_angle, float* g_rot, float* g_trans,
                      nr_stream_t stream);
+
+/* ---- batch assembly: RaySampler  (noisy_src/data.py:264-321) -----------
+ * out_*[b] = table_*[idx[b]] for the (n_rays,3) ray table (rays_o, rays_d,
+ * colors) in one launch; idx outside [0, n_rays) gives NaN rows.            */
+int nr_gather_rays(const int64_t* idx, int64_t n_rays, int B,
+                   const float* rays_o, const float* rays_d, const float* colors,
+                   float* out_o, float* out_d, float* out_rgb, nr_stream_t stream);
 
 /* ---- A5: sample_along_rays  (noisy_src/rays.py:145-210) ------------------
  * z (B,N); pts (B,N,3) nullable.  t_rand (B,N) nullable -> no perturbation. */

@@ -393,7 +393,7 @@ def train_step(model_coarse, model_fine, state: TrainState, rays_o, rays_d, targ
     torch.nn.utils.clip_grad_norm_(state.params, max_norm=max_norm)
     state.optimizer.step()
     state.scheduler.step()
-    return {"loss": float(loss), "loss_coarse": float(loss_coarse),
+    return {"loss": float(loss.detach()), "loss_coarse": float(loss_coarse.detach()),
             "loss_fine": None if loss_fine is None else float(loss_fine)}
 
 

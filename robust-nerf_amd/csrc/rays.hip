@@ -63,6 +63,69 @@ __global__ void get_rays_kernel(const float* dirs, const float* c2w, int64_t N, 
     ro[3 * p + 2] = c2w[11];
 }
 
+// A2 backward (rays.py:67-99 is differentiable w.r.t. c2w and the directions):
+// rays_d = v/|v|, v = R d  ->  g_v = (g_d - u (u.g_d)) / |v|,  g_R += g_v d^T,
+// g_d(dirs) = R^T g_v;  rays_o = t  ->  g_t += g_o.  The sum over the N rays is a
+// fixed-shape two-pass reduction (kGrBlocks partials of 12, then one block).
+constexpr int kGrBlocks = 256, kGrThreads = 256;
+
+__global__ void __launch_bounds__(kGrThreads)
+get_rays_bwd_partial_kernel(const float* dirs, const float* c2w, int64_t N, const float* g_ro, const float* g_rd,
+                            float* g_dirs, float* partials) {
+    const float* R = c2w;
+    float acc[12];
+    for (int e = 0; e < 12; ++e) acc[e] = 0.f;
+    for (int64_t p = static_cast<int64_t>(blockIdx.x) * kGrThreads + threadIdx.x; p < N;
+         p += static_cast<int64_t>(kGrBlocks) * kGrThreads) {
+        if (g_ro)
+            for (int r = 0; r < 3; ++r) acc[9 + r] += g_ro[3 * p + r];
+        if (!g_rd) continue;
+        const float d3[3] = {dirs[3 * p], dirs[3 * p + 1], dirs[3 * p + 2]};
+        const float vx = (d3[0] * R[0] + d3[1] * R[1]) + d3[2] * R[2];
+        const float vy = (d3[0] * R[4] + d3[1] * R[5]) + d3[2] * R[6];
+        const float vz = (d3[0] * R[8] + d3[1] * R[9]) + d3[2] * R[10];
+        const float n = norm3(vx, vy, vz);
+        const float ux = vx / n, uy = vy / n, uz = vz / n;
+        const float gx = g_rd[3 * p], gy = g_rd[3 * p + 1], gz = g_rd[3 * p + 2];
+        const float dot = ux * gx + uy * gy + uz * gz;
+        const float gv[3] = {(gx - ux * dot) / n, (gy - uy * dot) / n, (gz - uz * dot) / n};
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k) acc[3 * r + k] += gv[r] * d3[k];
+        if (g_dirs)
+            for (int k = 0; k < 3; ++k)
+                g_dirs[3 * p + k] = (R[k] * gv[0] + R[4 + k] * gv[1]) + R[8 + k] * gv[2];
+    }
+    __shared__ float part[12][kGrThreads / 64];
+    for (int e = 0; e < 12; ++e) {
+        float v = acc[e];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if ((threadIdx.x & 63) == 0) part[e][threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        float t = 0.f;
+        for (int w = 0; w < kGrThreads / 64; ++w) t += part[threadIdx.x][w];
+        partials[blockIdx.x * 12 + threadIdx.x] = t;
+    }
+}
+
+__global__ void __launch_bounds__(kGrThreads) get_rays_bwd_final_kernel(const float* partials, float* g_c2w) {
+    static_assert(kGrThreads == kGrBlocks, "one partial per thread");
+    __shared__ float part[12][kGrThreads / 64];
+    for (int e = 0; e < 12; ++e) {
+        float v = partials[threadIdx.x * 12 + e];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if ((threadIdx.x & 63) == 0) part[e][threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        const int e = threadIdx.x;
+        float t = 0.f;
+        for (int w = 0; w < kGrThreads / 64; ++w) t += part[e][w];
+        g_c2w[e < 9 ? 4 * (e / 3) + (e % 3) : 4 * (e - 9) + 3] += t;
+    }
+}
+
 // ---------------------------------------------------------------- A3 -----
 // Camera-frame direction of pixel (u,v): the reference gathers it from the
 // precomputed get_ray_directions table with .long() (truncating) indices.
@@ -298,6 +361,22 @@ __global__ void se3_poses_bwd_kernel(const float* init, const float* rot, const 
         for (int m = 0; m < 3; ++m) g_rot[3 * p + m] += sr[m];
 }
 
+// ------------------------------------------------ batch assembly (§8f-1) -
+// RaySampler (data.py:264-321): rows idx[b] of the device ray table (rays_o,
+// rays_d, colors; 36 B per ray) into one batch, one launch for all three.
+__global__ void gather_rays_kernel(const int64_t* idx, int64_t n_rays, int B, const float* ro, const float* rd,
+                                   const float* rgb, float* out_o, float* out_d, float* out_rgb) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int64_t i = idx[b];
+    const bool ok = i >= 0 && i < n_rays;
+    for (int c = 0; c < 3; ++c) {
+        out_o[3 * b + c] = ok ? ro[3 * i + c] : __builtin_nanf("");
+        out_d[3 * b + c] = ok ? rd[3 * i + c] : __builtin_nanf("");
+        out_rgb[3 * b + c] = ok ? rgb[3 * i + c] : __builtin_nanf("");
+    }
+}
+
 // ---------------------------------------------------------------- A5 -----
 __global__ void stratified_kernel(const float* ro, const float* rd, const float* t_rand, float near_,
                                   float far_, int lindisp, int B, int N, float* z_out, float* pts) {
@@ -450,6 +529,23 @@ int nr_get_rays(const float* dirs, const float* c2w, int64_t N, float* ro, float
     return NR_OK;
 }
 
+int64_t nr_get_rays_bwd_workspace_bytes(void) { return static_cast<int64_t>(kGrBlocks) * 12 * sizeof(float); }
+
+int nr_get_rays_bwd(const float* dirs, const float* c2w, int64_t N, const float* g_ro, const float* g_rd,
+                    float* g_dirs, float* g_c2w, void* workspace, nr_stream_t stream) {
+    NR_REQUIRE(dirs && c2w && g_c2w && workspace && N >= 0 && (g_ro || g_rd) && (!g_dirs || g_rd),
+               "nr_get_rays_bwd: bad arguments");
+    if (N == 0) return NR_OK;
+    float* partials = static_cast<float*>(workspace);
+    hipLaunchKernelGGL(get_rays_bwd_partial_kernel, dim3(kGrBlocks), dim3(kGrThreads), 0,
+                       static_cast<hipStream_t>(stream), dirs, c2w, N, g_ro, g_rd, g_dirs, partials);
+    NR_LAUNCH_CHECK("nr_get_rays_bwd");
+    hipLaunchKernelGGL(get_rays_bwd_final_kernel, dim3(1), dim3(kGrThreads), 0, static_cast<hipStream_t>(stream),
+                       partials, g_c2w);
+    NR_LAUNCH_CHECK("nr_get_rays_bwd");
+    return NR_OK;
+}
+
 int nr_rays_from_pixels_fwd(const int64_t* img_idx, const float* pix, const float* poses, int n_img, int H,
                             int W, float focal, int B, float* ro, float* rd, nr_stream_t stream) {
     NR_REQUIRE(img_idx && pix && poses && ro && rd && B >= 0 && n_img > 0, "nr_rays_from_pixels_fwd: bad arguments");
@@ -501,6 +597,17 @@ int nr_se3_poses_bwd(const float* init, const float* rot, const int64_t* indices
                        static_cast<hipStream_t>(stream), init, rot, indices, n, n_poses, g_poses, fixed_small, g_rot,
                        g_trans);
     NR_LAUNCH_CHECK("nr_se3_poses_bwd");
+    return NR_OK;
+}
+
+int nr_gather_rays(const int64_t* idx, int64_t n_rays, int B, const float* rays_o, const float* rays_d,
+                   const float* colors, float* out_o, float* out_d, float* out_rgb, nr_stream_t stream) {
+    NR_REQUIRE(idx && rays_o && rays_d && colors && out_o && out_d && out_rgb && B >= 0 && n_rays >= 0,
+               "nr_gather_rays: bad arguments");
+    if (B == 0) return NR_OK;
+    hipLaunchKernelGGL(gather_rays_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, static_cast<hipStream_t>(stream), idx,
+                       n_rays, B, rays_o, rays_d, colors, out_o, out_d, out_rgb);
+    NR_LAUNCH_CHECK("nr_gather_rays");
     return NR_OK;
 }
 

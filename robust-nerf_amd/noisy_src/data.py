@@ -9,7 +9,8 @@ Scene data and ray batches — drop-in for ShawnnnLiu/Robust-NeRF ``noisy_src/da
 * ``RayDataset`` builds the ray table on the device with the HIP ``get_rays`` kernel
   (data.py:161-261; 100 x 640k rays x 36 B = 2.3 GB at 800^2, resident in HBM).
 * ``RaySampler`` keeps the reference's epoch ``randperm`` sampler (data.py:264-321)
-  with the permutation and the gathers on the device: no host work per batch.
+  with the permutation on the device and the batch assembled by one HIP gather of
+  the ray table (``nr_gather_rays``): no host work per batch.
 """
 
 from __future__ import annotations
@@ -160,7 +161,8 @@ class RaySampler:
 
     def _gather(self, idx: torch.Tensor) -> dict:
         ds = self.dataset
-        return {"rays_o": ds.rays_o[idx], "rays_d": ds.rays_d[idx], "target_rgb": ds.colors[idx]}
+        o, d, rgb = ops.gather_rays(idx, ds.rays_o, ds.rays_d, ds.colors)
+        return {"rays_o": o, "rays_d": d, "target_rgb": rgb}
 
     def __next__(self) -> dict:
         if self.current_idx >= self.n_rays:

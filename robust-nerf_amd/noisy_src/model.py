@@ -121,6 +121,25 @@ class _MLPFunction(torch.autograd.Function):
         return (g_x, g_d, None, *grads)
 
 
+def _check_supported(cfg: NrMlpConfig, config: ModelConfig, n_params: int) -> None:
+    """Fail at construction, not at the first forward, for a ModelConfig the compiled
+    kernels do not cover.  The fused MLP (csrc/mlp.hip) is specialised for the
+    reference's width: hidden_dim 256 (8 MFMA row blocks of 32), pos_freqs <= 10
+    (x_enc in 2 k-blocks), dir_freqs <= 4 (d_enc in 1 k-block); any depth 1..16 and
+    any skip set.  The plan check is host code (nr_mlp_packed_bytes), so this runs
+    without a GPU."""
+    lib = _hip.load()
+    if int(lib.nr_mlp_packed_bytes(ctypes.byref(cfg))) < 0:
+        raise NotImplementedError(
+            f"ModelConfig(hidden_dim={config.hidden_dim}, pos_freqs={config.pos_freqs}, "
+            f"dir_freqs={config.dir_freqs}, num_hidden_layers={config.num_hidden_layers}, skips={config.skips}) "
+            f"is outside the envelope of the compiled MI355X kernels: {_hip.last_error()} "
+            "(supported: hidden_dim=256, pos_freqs<=10, dir_freqs<=4, 1..16 layers, any skips)")
+    want = int(lib.nr_mlp_param_count(ctypes.byref(cfg)))
+    if want != n_params:
+        raise RuntimeError(f"NeRF parameter layout mismatch: module {n_params} vs kernel plan {want}")
+
+
 class NeRF(nn.Module):
     """Reference model.py:83-196 (same submodules, parameter order and init)."""
 
@@ -156,6 +175,7 @@ class NeRF(nn.Module):
             n_layers=config.num_hidden_layers, skip_mask=skip_mask, use_view_dirs=int(bool(config.use_view_dirs)),
             precision=_precision_code(getattr(config, "precision", "fp32")))
         self._param_count = sum(p.numel() for p in self.parameters())
+        _check_supported(self._nr_cfg, config, self._param_count)
         self._flat: Optional[torch.Tensor] = None
         self._packed: Optional[torch.Tensor] = None
         self._packed_key = None

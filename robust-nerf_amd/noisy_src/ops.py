@@ -45,16 +45,52 @@ def ray_directions(H: int, W: int, focal: float, cx: float, cy: float, device) -
     return out
 
 
+class _GetRays(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, directions, c2w):
+        d, c = _c(directions), _c(c2w)
+        if c.shape[-2:] not in ((4, 4), (3, 4)):
+            raise ValueError(f"get_rays: c2w must be (4,4) or (3,4), got {tuple(c.shape)}")
+        shape = d.shape
+        ro = torch.empty(shape, device=d.device, dtype=_f32)
+        rd = torch.empty(shape, device=d.device, dtype=_f32)
+        call("nr_get_rays", ptr(d), ptr(c), d.numel() // 3, ptr(ro), ptr(rd), _stream())
+        ctx.save_for_backward(d, c)
+        ctx.set_materialize_grads(False)
+        return ro, rd
+
+    @staticmethod
+    def backward(ctx, g_ro, g_rd):
+        d, c = ctx.saved_tensors
+        if g_ro is None and g_rd is None:
+            return None, None
+        g4 = torch.zeros(4, 4, device=c.device, dtype=_f32)
+        g_dirs = torch.empty_like(d) if (ctx.needs_input_grad[0] and g_rd is not None) else None
+        ws = torch.empty(int(_hip.load().nr_get_rays_bwd_workspace_bytes()), device=c.device, dtype=torch.uint8)
+        call("nr_get_rays_bwd", ptr(d), ptr(c), d.numel() // 3, ptr(_c(g_ro)), ptr(_c(g_rd)), ptr(g_dirs), ptr(g4),
+             ptr(ws), _stream())
+        g_c = g4[: c.shape[-2]] if ctx.needs_input_grad[1] else None
+        if g_dirs is None and ctx.needs_input_grad[0]:
+            g_dirs = torch.zeros_like(d)
+        return g_dirs, g_c
+
+
 def get_rays(directions: torch.Tensor, c2w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """rays.py:67-99; differentiable w.r.t. c2w and the directions, like the reference."""
     _check(directions, c2w)
-    d = _c(directions)
-    c = _c(c2w)
-    shape = d.shape
-    n = d.numel() // 3
-    ro = torch.empty(shape, device=d.device, dtype=_f32)
-    rd = torch.empty(shape, device=d.device, dtype=_f32)
-    call("nr_get_rays", ptr(d), ptr(c), n, ptr(ro), ptr(rd), _stream())
-    return ro, rd
+    return _GetRays.apply(directions, c2w)
+
+
+def gather_rays(idx, rays_o, rays_d, colors):
+    """RaySampler batch assembly (data.py:264-321): the rows idx of the device ray table,
+    all three arrays in one kernel."""
+    _check(idx, rays_o, rays_d, colors)
+    i = idx.to(torch.int64).contiguous()
+    B = i.shape[0]
+    out = [torch.empty(B, 3, device=i.device, dtype=_f32) for _ in range(3)]
+    call("nr_gather_rays", ptr(i), rays_o.shape[0], B, ptr(_c(rays_o)), ptr(_c(rays_d)), ptr(_c(colors)),
+         ptr(out[0]), ptr(out[1]), ptr(out[2]), _stream())
+    return out
 
 
 # ---------------------------------------------------------------- A5 / A9 / A10

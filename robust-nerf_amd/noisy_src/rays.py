@@ -35,9 +35,8 @@ def get_ray_directions(H: int, W: int, focal: float, center: Tuple[float, float]
 
 
 def get_rays(directions: torch.Tensor, c2w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Reference rays.py:67-99 -> (rays_o, rays_d), rays_d normalised."""
-    if c2w.requires_grad:
-        raise NotImplementedError("get_rays: differentiable poses go through PixelSampler.get_rays_for_batch")
+    """Reference rays.py:67-99 -> (rays_o, rays_d), rays_d normalised; differentiable
+    w.r.t. c2w (and the directions), as data_pose_opt.py:83-148 relies on."""
     if directions.device != c2w.device:
         directions = directions.to(c2w.device)
     return ops.get_rays(directions, c2w)

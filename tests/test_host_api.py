@@ -143,3 +143,16 @@ def test_hot_path_refuses_cpu_tensors():
     cam = CameraPoseParameters(torch.eye(4).expand(3, 4, 4).clone())
     with pytest.raises(Exception):
         cam.get_all_poses()
+
+
+def test_model_config_envelope_is_checked_at_construction():
+    """ModelConfigs the compiled kernels do not cover raise NotImplementedError when the
+    NeRF is built (reference model.py:98-143 builds any width); depth and skips are free."""
+    from noisy_src.config import ModelConfig
+    from noisy_src.model import NeRF
+    for kw in (dict(hidden_dim=128), dict(hidden_dim=512), dict(pos_freqs=11), dict(dir_freqs=5)):
+        with pytest.raises(NotImplementedError, match="envelope"):
+            NeRF(ModelConfig(**kw))
+    for kw in (dict(num_hidden_layers=4, skips=(1, 2)), dict(pos_freqs=6, dir_freqs=2), dict(skips=()),
+               dict(use_view_dirs=False)):
+        NeRF(ModelConfig(**kw))

@@ -240,3 +240,49 @@ def test_mse():
     lt.backward()
     assert abs(loss.item() - lt.item()) < 1e-7
     assert torch.allclose(gr.cpu(), at.grad, atol=1e-9)
+
+
+def test_get_rays_differentiable_in_c2w():
+    """A2 backward: rays.py:67-99 is differentiable w.r.t. c2w (and the directions); the
+    HIP backward matches autograd through the oracle (fp64) for a full 64x48 image."""
+    from noisy_src.rays import get_rays
+    pose = _gt_poses()[3]
+    dirs = ref.get_ray_directions(48, 64, 55.0)
+    g = torch.Generator().manual_seed(31)
+    go, gd = torch.randn(48, 64, 3, generator=g), torch.randn(48, 64, 3, generator=g)
+    for shape in ((4, 4), (3, 4)):
+        c = pose[: shape[0]].clone().to(DEV).requires_grad_(True)
+        dd = dirs.clone().to(DEV).requires_grad_(True)
+        o, d = get_rays(dd, c)
+        ((o * go.to(DEV)).sum() + (d * gd.to(DEV)).sum()).backward()
+        c64 = pose[: shape[0]].double().requires_grad_(True)
+        d64 = dirs.double().requires_grad_(True)
+        wo, wd = ref.get_rays(d64, c64)
+        ((wo * go.double()).sum() + (wd * gd.double()).sum()).backward()
+        assert (o.detach().cpu() - wo.detach()).abs().max() < 1e-6
+        assert (d.detach().cpu() - wd.detach()).abs().max() < 1e-6
+        assert torch.allclose(c.grad.cpu().double(), c64.grad, rtol=1e-4, atol=1e-4), (c.grad, c64.grad)
+        assert torch.allclose(dd.grad.cpu().double(), d64.grad, rtol=1e-4, atol=1e-4)
+    # rays_o only (the pose-translation path) and bit-reproducibility
+    outs = []
+    for _ in range(2):
+        c = pose.clone().to(DEV).requires_grad_(True)
+        o, _ = get_rays(dirs.to(DEV), c)
+        (o * go.to(DEV)).sum().backward()
+        outs.append(c.grad.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.allclose(outs[0][:3, 3], go.reshape(-1, 3).sum(0), rtol=1e-4)
+
+
+def test_gather_rays_matches_indexing():
+    """RaySampler batch assembly (data.py:264-321): one gather launch == table[idx]."""
+    from noisy_src import ops
+    g = torch.Generator().manual_seed(41)
+    n, B = 10007, 4096
+    o, d, c = (torch.randn(n, 3, generator=g).to(DEV) for _ in range(3))
+    idx = torch.randint(0, n, (B,), generator=g).to(DEV)
+    go, gd, gc = ops.gather_rays(idx, o, d, c)
+    assert torch.equal(go, o[idx]) and torch.equal(gd, d[idx]) and torch.equal(gc, c[idx])
+    bad = idx.clone()
+    bad[5] = n
+    go, _, _ = ops.gather_rays(bad, o, d, c)
+    assert torch.isnan(go[5]).all() and torch.equal(go[6:], o[idx[6:]])
