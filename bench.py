@@ -132,8 +132,10 @@ def psnr_record():
             "commit": rec.get("commit"), "scene": rec.get("scene", "analytic 3-sphere scene, lego train cameras"),
             "iters": rec["iters"], "seeds": rec["seeds"],
             "mean_db": {k: round(v["mean"], 3) for k, v in rec["summary"].items()},
-            "delta_db_vs_ref": {k: v["delta_mean_db"] for k, v in rec["delta_vs_ref"].items()},
-            "se_of_delta_db": {k: v["se_of_delta_db"] for k, v in rec["delta_vs_ref"].items()}}
+            "lr_decay": rec.get("lr_decay"),
+            "paired_delta_db_vs_ref": {k: v.get("paired_mean_db", v["delta_mean_db"])
+                                       for k, v in rec["delta_vs_ref"].items()},
+            "paired_se_db": {k: v.get("paired_se_db", v["se_of_delta_db"]) for k, v in rec["delta_vs_ref"].items()}}
 
 
 def _cpu_model() -> str:

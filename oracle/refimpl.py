@@ -394,7 +394,7 @@ def train_step(model_coarse, model_fine, state: TrainState, rays_o, rays_d, targ
     state.optimizer.step()
     state.scheduler.step()
     return {"loss": float(loss.detach()), "loss_coarse": float(loss_coarse.detach()),
-            "loss_fine": None if loss_fine is None else float(loss_fine)}
+            "loss_fine": None if loss_fine is None else float(loss_fine.detach())}
 
 
 def flat_params(model: nn.Module) -> torch.Tensor:

@@ -12,7 +12,13 @@ weights and see the same ray batches and the same stratified / inverse-CDF draws
 * ``hip``  — this package's engine.Trainer (HIP kernels, fused clip + Adam), fp32 or bf16.
 
 Test PSNR is the mean over the test views of -10 log10(MSE) of deterministic renders.
-``python tests/psnr_parity.py [iters] [size] [seeds]`` writes profiles/r01_psnr_parity.json.
+``python tests/psnr_parity.py [iters] [size] [seeds] [out.json] [lr_decay]`` writes the
+record (default profiles/r02_psnr_parity.json).  ``lr_decay`` is the reference's
+TrainConfig.lr_decay (LambdaLR 0.1^(step / (lr_decay * 1000)), train.py:405-411): at the
+default 250 the LR is constant over a short run and the final PSNR of two runs that
+differ by one rounding keeps fluctuating chaotically by ~0.7 dB; lr_decay = 1 anneals
+the LR 100x over 2000 iterations, which settles both trajectories and makes the
+equal-iteration comparison resolvable.
 """
 
 from __future__ import annotations
@@ -69,7 +75,7 @@ def render_gt(o, d):
     return ref.raw2outputs(rgb, sigma[..., None], z, d, white_background=True)["rgb_map"]
 
 
-def run(impl: str, precision: str, iters: int, size: int, batch: int, seed: int = 0, log=None):
+def run(impl: str, precision: str, iters: int, size: int, batch: int, seed: int = 0, log=None, lr_decay: int = 250):
     from noisy_src.config import ModelConfig, RenderConfig
     dev = torch.device("cuda")
     poses, focal = camera(size)
@@ -81,7 +87,7 @@ def run(impl: str, precision: str, iters: int, size: int, batch: int, seed: int 
     oc, of = ref.create_nerf(ModelConfig(precision="fp32"))
     if impl == "ref":
         mc, mf = oc.to(dev), of.to(dev)
-        state = ref.TrainState(mc, mf)
+        state = ref.TrainState(mc, mf, lr_decay=lr_decay)
     else:
         from noisy_src.engine import Trainer
         from noisy_src.model import create_nerf
@@ -89,7 +95,7 @@ def run(impl: str, precision: str, iters: int, size: int, batch: int, seed: int 
         mc.load_state_dict(oc.state_dict())
         mf.load_state_dict(of.state_dict())
         mc, mf = mc.to(dev), mf.to(dev)
-        trainer = Trainer(mc, mf, rc)
+        trainer = Trainer(mc, mf, rc, lr_decay=lr_decay)
     g = torch.Generator().manual_seed(seed)
     t0 = time.time()
     for it in range(iters):
@@ -125,25 +131,70 @@ def summarize(runs):
             "runs": [round(x, 4) for x in v.tolist()]}
 
 
+IMPLS = (("ref", "fp32"), ("hip", "fp32"), ("hip", "bf16"))
+
+
+def worker(iters, size, batch, lr_decay, seeds, out_file):
+    """Run every implementation on ``seeds``; one JSON line per run into out_file."""
+    with open(out_file, "w") as fh:
+        for sd in seeds:
+            for impl, prec in IMPLS:
+                r = run(impl, prec, iters, size, batch, seed=sd, lr_decay=lr_decay,
+                        log=lambda m, sd=sd: print(f"seed {sd}: {m}", flush=True))  # heartbeat
+                r["seed"] = sd
+                fh.write(json.dumps(r) + "\n")
+                fh.flush()
+                print(f"{impl}/{prec} seed {sd}: {r['test_psnr']:.3f} dB ({r['train_seconds']} s)", flush=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--from-log":
+        from_log(sys.argv[2], Path(sys.argv[3]), note=sys.argv[4] if len(sys.argv) > 4 else None)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "--worker":
+        it, size, batch, lr_decay = (int(v) for v in sys.argv[2:6])
+        worker(it, size, batch, lr_decay, [int(v) for v in sys.argv[7].split(",")], sys.argv[6])
+        return
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
     size = int(sys.argv[2]) if len(sys.argv) > 2 else 64
     n_seeds = int(sys.argv[3]) if len(sys.argv) > 3 else 6
-    out_path = Path(sys.argv[4]) if len(sys.argv) > 4 else ROOT / "profiles" / "r01_psnr_parity.json"
+    out_path = Path(sys.argv[4]) if len(sys.argv) > 4 else ROOT / "profiles" / "r02_psnr_parity.json"
+    lr_decay = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+    n_workers = int(sys.argv[6]) if len(sys.argv) > 6 else 1
     batch = 1024
     # Training at constant Adam LR is chaotic: a 1-ulp difference anywhere decorrelates two
     # trajectories within a few hundred steps, so one run of each says nothing at 0.1 dB.
     # Each implementation trains on the same n_seeds batch/draw streams from the same
-    # init, and the means are compared against the reference's own seed-to-seed spread.
+    # init, and the difference is taken per seed (paired) and over the seeds.  The
+    # oracle's eager-torch step is launch-bound, so seeds run in n_workers processes that
+    # share the GPU (each run is independent and deterministic given its seed).
+    import subprocess
+    import tempfile
+    tmp = Path(tempfile.mkdtemp())
+    procs = []
+    for w in range(n_workers):
+        seeds = list(range(w, n_seeds, n_workers))
+        if seeds:
+            procs.append(subprocess.Popen([sys.executable, "-u", __file__, "--worker", str(iters), str(size),
+                                           str(batch), str(lr_decay), str(tmp / f"w{w}.jsonl"),
+                                           ",".join(map(str, seeds))]))
+    rcs = [pr.wait() for pr in procs]
+    if any(rcs):
+        raise SystemExit(f"psnr_parity workers failed: {rcs}")
+    results = [json.loads(line) for f in sorted(tmp.glob("w*.jsonl")) for line in f.read_text().splitlines()]
+    summarize_results(results, iters, size, batch, n_seeds, lr_decay, out_path)
+
+
+def summarize_results(results, iters, size, batch, n_seeds, lr_decay, out_path, note=None):
+    """Paired statistics over the seeds every implementation completed; writes out_path."""
+    complete = set.intersection(*[{r["seed"] for r in results if (r["impl"], r["precision"]) == ip}
+                                  for ip in IMPLS])
+    results = [r for r in results if r["seed"] in complete]
+    n_seeds = len(complete)
     groups = {}
-    for impl, prec in (("ref", "fp32"), ("hip", "fp32"), ("hip", "bf16")):
-        runs = []
-        for sd in range(n_seeds):
-            r = run(impl, prec, iters, size, batch, seed=sd, log=None)
-            r["seed"] = sd
-            runs.append(r)
-            print(f"{impl}/{prec} seed {sd}: {r['test_psnr']:.3f} dB ({r['train_seconds']} s)", flush=True)
-        groups[f"{impl}_{prec}"] = runs
+    for impl, prec in IMPLS:
+        groups[f"{impl}_{prec}"] = sorted((r for r in results if r["impl"] == impl and r["precision"] == prec),
+                                          key=lambda r: r["seed"])
     summ = {k: summarize(v) for k, v in groups.items()}
     base = summ["ref_fp32"]
     delta = {}
@@ -151,19 +202,49 @@ def main():
         d = summ[k]["mean"] - base["mean"]
         se = math.sqrt(summ[k]["sem"] ** 2 + base["sem"] ** 2)
         paired = [a["test_psnr"] - b["test_psnr"] for a, b in zip(groups[k], groups["ref_fp32"])]
+        pse = float(np.std(paired, ddof=1) / math.sqrt(len(paired))) if len(paired) > 1 else 0.0
         delta[k] = {"delta_mean_db": round(d, 4), "se_of_delta_db": round(se, 4),
+                    "paired_mean_db": round(float(np.mean(paired)), 4), "paired_se_db": round(pse, 4),
                     "z": round(d / se, 3) if se > 0 else None,
                     "paired_deltas_db": [round(x, 4) for x in paired]}
+    import os
+    import subprocess
+    commit = os.environ.get("NR_COMMIT")  # the GPU box gets the tree without .git
+    if not commit:
+        try:
+            commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+                                    cwd=ROOT).stdout.strip() or None
+        except OSError:
+            commit = None
     out = {"what": "test PSNR after equal iterations, identical init; seed = batch and random-draw stream; "
                    "analytic 3-sphere scene from the lego training cameras (90 train, 10 test views); "
-                   "64c+128f, Adam 5e-4, batch 1024; n seeds per implementation",
-           "iters": iters, "size": size, "batch": batch, "seeds": n_seeds,
+                   f"64c+128f, Adam 5e-4, LambdaLR lr_decay={lr_decay}, batch 1024; n seeds per implementation",
+           "scene": "analytic 3-sphere scene, lego train cameras (90 train / 10 test views)",
+           "commit": commit, "lr_decay": lr_decay,
+           "iters": iters, "size": size, "batch": batch, "seeds": n_seeds, "note": note,
            "summary": summ, "delta_vs_ref": delta,
            "results": [r for v in groups.values() for r in v]}
     out_path.parent.mkdir(parents=True, exist_ok=True)
     out_path.write_text(json.dumps(out, indent=1))
     print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "runs"} for k, v in summ.items()}))
     print(json.dumps(delta))
+
+
+
+
+def from_log(log_path, out_path, iters=2000, size=64, batch=1024, lr_decay=1, note=None):
+    """Rebuild the record from a run log's per-run lines ("impl/prec seed s: X dB (t s)")."""
+    import re
+    pat = re.compile(r"^(ref|hip)/(fp32|bf16) seed (\d+): ([0-9.]+) dB \(([0-9.]+) s\)")
+    results = []
+    for line in Path(log_path).read_text().splitlines():
+        m = pat.match(line)
+        if m:
+            results.append({"impl": m[1], "precision": m[2], "seed": int(m[3]), "test_psnr": float(m[4]),
+                            "per_view": None, "iters": iters, "batch": batch, "size": size,
+                            "train_seconds": float(m[5])})
+    summarize_results(results, iters, size, batch, None, lr_decay, out_path, note=note)
+
 
 
 if __name__ == "__main__":
