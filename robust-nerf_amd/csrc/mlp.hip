@@ -670,20 +670,24 @@ __device__ __forceinline__ void epi16_blk(const f32x16& a, bf16x8 (&out)[2], uns
     }
 }
 
-template <int PREC, bool RELU, bool MASK, class Dst>
+template <int PREC, int TPW, bool RELU, bool MASK, class Dst>
 struct LayerEpi {
     static constexpr bool kOn = true;
-    f32x16* acc;      // the layer's accumulators (one tile)
-    const float* bl;  // bias, lane < 32 holds row 32 nb + lane
-    Dst* dst;         // where the 16-bit output blocks go (LDS activations)
-    unsigned* mw;     // mask words (MASK)
+    f32x16 (*acc)[kHB];  // the layer's accumulators, acc[TPW][kHB]
+    const float* bl;     // bias, lane < 32 holds row 32 nb + lane
+    Dst* dst;            // where the 16-bit output blocks go (activations)
+    unsigned (*mw)[4];   // mask words per tile (MASK)
     __device__ __forceinline__ void bias(int nb) const {
-        acc[nb] = mfma16<PREC>(bias_frag<PREC>(bl[nb]), ones16<PREC>(), acc[nb]);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) acc[t][nb] = mfma16<PREC>(bias_frag<PREC>(bl[nb]), ones16<PREC>(), acc[t][nb]);
     }
     __device__ __forceinline__ void finish(int nb) const {
-        bf16x8 o[2];
-        epi16_blk<PREC, RELU, MASK>(acc[nb], o, mw, nb);
-        dst->put(0, nb, InBlk<PREC>{{o[0], o[1]}});
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            bf16x8 o[2];
+            epi16_blk<PREC, RELU, MASK>(acc[t][nb], o, mw[t], nb);
+            dst->put(t, nb, InBlk<PREC>{{o[0], o[1]}});
+        }
     }
 };
 
@@ -697,7 +701,7 @@ __device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1]
                                             const StreamDesc& sd, int tid, int lane,
                                             const Sink<PREC, TPW>& sink = Sink<PREC, TPW>{nullptr, 0, 0, 0u},
                                             const Epi& epi = Epi{}) {
-    static_assert(!Epi::kOn || (k16<PREC> && TPW == 1 && N2 == 0), "epilogue hook: 16-bit, one tile");
+    static_assert(!Epi::kOn || (k16<PREC> && N2 == 0), "epilogue hook: 16-bit");
     // Chunk sizes, read once per segment: every chunk of a segment has this
     // segment's size; the prefetch in its last step is the next segment's first chunk.
     const int q0 = ring.q;
@@ -862,12 +866,12 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     stream_begin(ring, st, a.packed, a.sd, tid);
 
     f32x16 acc[TPW][kHB];
-    constexpr bool ACT_LDS = k16<PREC> && NT == 512;
+    constexpr bool ACT_LDS = k16<PREC> && (NT == 512 || TPW >= 2);
     Act<PREC, TPW, kHB, ACT_LDS> hin;
     if constexpr (ACT_LDS)
         hin.base = lds + 2 * a.slot_bytes + wv * Act<PREC, TPW, kHB, ACT_LDS>::kBytes;
     f32x16 dummy[TPW][1];
-    unsigned w[4];
+    unsigned w[TPW][4];
     for (int i = 0; i < n; ++i) {
 #pragma unroll
         for (int t = 0; t < TPW; ++t)
@@ -878,12 +882,14 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) bl[nb] = lane < 32 ? a.params[a.bo[i] + 32 * nb + lane] : 0.f;
         const bool skip_in = i > 0 && ((a.skips >> (i - 1)) & 1u);
-        // 16-bit, one tile per wave: the epilogue runs inside the layer's last chunk
-        constexpr bool HOOK = k16<PREC> && TPW == 1 && NR_EPI_HOOK;
+        // 16-bit: the epilogue runs inside the layer's last chunk
+        constexpr bool HOOK = k16<PREC> && NR_EPI_HOOK;
         if constexpr (HOOK)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) w[q] = 0u;
-        const LayerEpi<PREC, true, TRAIN, decltype(hin)> ep{acc[0], bl, &hin, w};
+            for (int t = 0; t < TPW; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) w[t][q] = 0u;
+        const LayerEpi<PREC, TPW, true, TRAIN, decltype(hin)> ep{acc, bl, &hin, w};
         if (i == 0 || skip_in) {
             // x_enc is not kept in registers: the skip layer reloads the saved
             // copy (training) or recomputes it (inference)
@@ -950,11 +956,11 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                     unsigned wt[4];
                     bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[i], lane), wt);
                 }
-                epi16<PREC, kHB, true, false, TRAIN>(acc[t], hv, w);
+                epi16<PREC, kHB, true, false, TRAIN>(acc[t], hv, w[t]);
 #pragma unroll
                 for (int nb = 0; nb < kHB; ++nb) hin.put(t, nb, InBlk<PREC>{{hv[nb][0], hv[nb][1]}});
             } else {
-                bias_act<kHB, true>(acc[t], vimg(a.packed, a.vb[i], lane), w);
+                bias_act<kHB, true>(acc[t], vimg(a.packed, a.vb[i], lane), w[t]);
 #pragma unroll
                 for (int nb = 0; nb < kHB; ++nb) {
                     InBlk<PREC> v;
@@ -963,7 +969,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                 }
             }
             if constexpr (TRAIN)
-                if (tok[t]) masks[((tile0 + t) * a.n_mask + i) * 64 + lane] = u32x4{w[0], w[1], w[2], w[3]};
+                if (tok[t]) masks[((tile0 + t) * a.n_mask + i) * 64 + lane] = u32x4{w[t][0], w[t][1], w[t][2], w[t][3]};
         }
     }
 
@@ -994,12 +1000,12 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     for (int t = 0; t < TPW; ++t)
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb) zero(acc[t][nb]);
-    constexpr bool HOOKF = k16<PREC> && TPW == 1 && NR_EPI_HOOK;
+    constexpr bool HOOKF = k16<PREC> && NR_EPI_HOOK;
     if constexpr (HOOKF) {
         float bf[kHB];
 #pragma unroll
         for (int nb = 0; nb < kHB; ++nb) bf[nb] = lane < 32 ? a.params[a.bo[n] + 32 * nb + lane] : 0.f;
-        const LayerEpi<PREC, false, false, decltype(hin)> epf{acc[0], bf, &hin, w};
+        const LayerEpi<PREC, TPW, false, false, decltype(hin)> epf{acc, bf, &hin, w};
         stream_gemm<PREC, TPW, kHB, 0, kHB, G, NT>(acc, dummy, 0, hin, ring, st, a.packed, a.sd, tid, lane,
                                                    sink_of(SV_H0 + n - 1, kHB), epf);
     } else {
@@ -1021,11 +1027,11 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                 unsigned wt[4];
                 bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[n], lane), wt);
             }
-            epi16<PREC, kHB, false, false, false>(acc[t], hv, w);
+            epi16<PREC, kHB, false, false, false>(acc[t], hv, w[t]);
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) hin.put(t, nb, InBlk<PREC>{{hv[nb][0], hv[nb][1]}});
         } else {
-            bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[n], lane), w);
+            bias_act<kHB, false>(acc[t], vimg(a.packed, a.vb[n], lane), w[t]);
 #pragma unroll
             for (int nb = 0; nb < kHB; ++nb) {
                 InBlk<PREC> v;
@@ -1081,9 +1087,9 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                 unsigned wt[4];
                 bias_act<NC, false>(ac[t], vimg(a.packed, a.vb[n + 1], lane), wt);
             }
-            epi16<PREC, NC, true, true, TRAIN>(ac[t], hcv, w);
+            epi16<PREC, NC, true, true, TRAIN>(ac[t], hcv, w[t]);
         } else {
-            bias_act<NC, true>(ac[t], vimg(a.packed, a.vb[n + 1], lane), w);
+            bias_act<NC, true>(ac[t], vimg(a.packed, a.vb[n + 1], lane), w[t]);
         }
         if constexpr (TRAIN) {
             if (tok[t]) {
@@ -1096,7 +1102,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                         to_in<PREC>(ac[t][nb], v);
                     store_img<PREC>(a.saved + a.sv_off[a.sv_hc], tile0 + t, NC, nb, v, lane);
                 }
-                masks[((tile0 + t) * a.n_mask + n) * 64 + lane] = u32x4{w[0], w[1], w[2], w[3]};
+                masks[((tile0 + t) * a.n_mask + n) * 64 + lane] = u32x4{w[t][0], w[t][1], w[t][2], w[t][3]};
             }
         }
         // rgb head (VALU): sigmoid(W_rgb h_c + b)
@@ -1875,7 +1881,7 @@ int launch_fwd(const MlpPlan& p, FwdArgs& a, hipStream_t s) {
         return NR_EARG;
     }
     a.slot_bytes = mc;
-    constexpr bool ACT_LDS = k16<PREC> && NT == 512;
+    constexpr bool ACT_LDS = k16<PREC> && (NT == 512 || TPW >= 2);
     const size_t lds = 2 * static_cast<size_t>(mc) + (ACT_LDS ? (NT / 64) * TPW * kHB * 2 * kFragBytes : 0);
     if (lds > 160 * 1024) {
         set_error("nr_mlp_forward: %zu bytes of LDS exceed 160 KiB", lds);

@@ -43,10 +43,18 @@ def main():
     B = 256
     per = B // world
     sl = slice(rank * per, (rank + 1) * per)
+    pose_grads = []
     if pose_mode:
         # joint pose optimisation (cfg #3): the pose gradient is one more all-reduce
         cam, sampler = pose_opt_setup(64, 64, dev)
         trainer = PoseTrainer(mc, mf, cam, sampler, rc, process_group=pg)
+        orig = trainer.optimizer_poses.step
+
+        def capture(*a, **k):  # the (all-reduced) pose gradient right before the pose Adam
+            pose_grads.append(torch.cat([p.grad.reshape(-1) for p in cam.parameters()]).cpu())
+            return orig(*a, **k)
+
+        trainer.optimizer_poses.step = capture
     else:
         trainer = Trainer(mc, mf, rc, process_group=pg)
     for k in range(steps):
@@ -63,6 +71,7 @@ def main():
     flat = torch.cat([mc.flat_params().cpu(), mf.flat_params().cpu()])
     if pose_mode:
         flat = torch.cat([flat, torch.cat([p.detach().reshape(-1).cpu() for p in cam.parameters()])])
+        torch.save(torch.stack(pose_grads), out / f"pose_grads_rank{rank}_of{world}.pt")
     torch.save(flat, out / f"{'pose_' if pose_mode else ''}rank{rank}_of{world}.pt")
     if pg is not None:
         dist.destroy_process_group()
