@@ -252,6 +252,40 @@ __device__ __forceinline__ float pe_fast(const PeRev& p, int f0, int f1, bool h1
     return h1 ? a1 : a0;
 }
 
+// Backward of pe_fast: d gamma_f / d x_c contracted with g, for feature f0 (lane
+// half 0) / f1 (half 1).  d sin(theta + phi)/d theta = sin(theta + phi + 1/4 rev), so
+// the derivative is the same hardware sine a quarter revolution on (sin -> cos,
+// cos -> -sin), times 2^k.  16-bit paths only (the fp32 path keeps sinf/cosf).
+__device__ __forceinline__ void pe_fast_bwd(const PeRev& p, int f0, int f1, bool h1, int L, float g, float& g0,
+                                            float& g1, float& g2) {
+    auto chan = [](int f) { return f < 3 ? f : ((f - 3) - 6 * ((f - 3) / 6)) % 3; };
+    auto live = [&](int f) { return f < 3 || (f - 3) / 6 < L; };
+    auto dgamma = [&](int f) -> float {  // d gamma_f / d x_c (f >= 3, live)
+        const int fp = f - 3, k = fp / 6, rem = fp - 6 * k, c = rem % 3;
+        const float sc = static_cast<float>(1 << (k < 24 ? k : 0));
+        const float hi = p.hi[c] * sc, lo = fmaf(p.lo[c], sc, rem < 3 ? 0.25f : 0.5f);
+        return __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(hi) + lo) * sc;
+    };
+    float d;
+    if (f0 >= 3 && f1 >= 3) {
+        const int fp0 = f0 - 3, k0 = fp0 / 6, r0 = fp0 - 6 * k0;
+        const int fp1 = f1 - 3, k1 = fp1 / 6, r1 = fp1 - 6 * k1;
+        const float s0 = static_cast<float>(1 << (k0 < 24 ? k0 : 0)), s1 = static_cast<float>(1 << (k1 < 24 ? k1 : 0));
+        const float hi = h1 ? p.hi[r1 % 3] * s1 : p.hi[r0 % 3] * s0;
+        const float lo = h1 ? fmaf(p.lo[r1 % 3], s1, r1 < 3 ? 0.25f : 0.5f) : fmaf(p.lo[r0 % 3], s0, r0 < 3 ? 0.25f : 0.5f);
+        d = g * (__builtin_amdgcn_sinf(__builtin_amdgcn_fractf(hi) + lo) * (h1 ? s1 : s0));
+    } else {
+        const float a0 = f0 < 3 ? 1.f : (live(f0) ? dgamma(f0) : 0.f);
+        const float a1 = f1 < 3 ? 1.f : (live(f1) ? dgamma(f1) : 0.f);
+        d = g * (h1 ? a1 : a0);
+    }
+    if (!(h1 ? live(f1) : live(f0))) return;
+    const int c = h1 ? chan(f1) : chan(f0);
+    g0 += c == 0 ? d : 0.f;
+    g1 += c == 1 ? d : 0.f;
+    g2 += c == 2 ? d : 0.f;
+}
+
 // ---- bf16 epilogue: bias by MFMA, ReLU and mask bits on packed bf16 pairs ----
 // Bias of row block nb as an MFMA A fragment against an all-ones B operand:
 // lanes 0..31 hold bias[32 nb + lane] split exactly into bf16 hi + mid + lo,
@@ -493,6 +527,9 @@ struct Ring {
 
 #ifndef NR_SINK_BWD
 #define NR_SINK_BWD 0  // 1: store each dz while the next stream consumes it (measured slower: 1.50 vs 1.35 ms)
+#endif
+#ifndef NR_DIN_FUSED
+#define NR_DIN_FUSED 0  // 1: 16-bit g_x / g_d through the 4-wave input-gradient dX variant (A/B)
 #endif
 #ifndef NR_STAGE_GLDS
 #define NR_STAGE_GLDS 1
@@ -1402,6 +1439,154 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     }
 }
 
+// ------------------------------------------------ input gradients ------
+// dL/dx and dL/dd of the 16-bit path (the pose-optimisation gradient, BASELINE
+// cfg #3) as a separate pass over the dz images the dX chain stores anyway:
+//   d x_enc = sum over the x_enc-reading layers l (0 and every skip layer) of
+//             W_l[:, x_enc]^T dz_l,        d d_enc = W_dir[:, d_enc]^T dz_dir,
+// then the positional-encoding backward.  Replaces the input-gradient variant of
+// mlp_bwd_kernel, which carries d x_enc through the whole trunk and therefore runs
+// 4 waves per CU (2.23 ms vs 1.17 ms for the plain dX chain).
+// One wave per 32-sample tile; the A fragments are the W^T images' x_enc / d_enc
+// row blocks (gathered into LDS once per workgroup), the B operands the stored dz
+// blocks.  fp32 accumulation, the same products as the fused variant.  HBM-bound:
+// 1.28 KB of dz per sample for the default model (dz_0, dz_skip, dz_c).
+struct DinArgs {
+    const char* packed;
+    const char* ws;
+    const float* x;
+    const float* d;
+    float* g_x;
+    float* g_d;
+    int64_t M, tiles;
+    int L, Ld;
+    float inv_gscale;
+    int nsrc;                     // x_enc-reading layers
+    int64_t a_off[kMaxTrunk];     // byte offset of the layer's W^T image
+    int a_kb[kMaxTrunk];          // row blocks per chunk of that image
+    int a_p0[kMaxTrunk];          // first x_enc row block within a chunk
+    int64_t dz_off[kMaxTrunk];    // byte offset of the layer's dz image in ws
+    int64_t dir_a_off, dz_dir_off;
+    int dir_kb, dir_p0, nc;       // dir W^T chunk rows, first d_enc row, dz_dir blocks
+};
+
+constexpr int kDinNT = 512;
+
+// The x_enc / d_enc row blocks of every source W^T image, gathered fragment by
+// fragment: [source][dz block][row block][2] then [dz_c block][row block][2] (1 KB each).
+__host__ __device__ inline int din_frags(int nsrc, int XB, int DB, int nc) { return 2 * (nsrc * kHB * XB + nc * DB); }
+
+template <int PREC, int XB, int DB, bool ALDS>
+__global__ __launch_bounds__(kDinNT) void mlp_dinput_kernel(DinArgs a) {
+    static_assert(k16<PREC>, "16-bit images only");
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int lane = threadIdx.x & 63, h = lane >> 5, ml = lane & 31;
+    // A operands: staged once per workgroup into LDS (72 KB for the default model), or
+    // read from the L2-resident packed buffer when they do not fit
+    auto frag_src = [&](int f) -> const char* {  // global address of gathered fragment f (lane 0)
+        const int nx = 2 * a.nsrc * kHB * XB;
+        if (f < nx) {
+            const int s = f / (2 * kHB * XB), r = f % (2 * kHB * XB);
+            const int ob = r / (2 * XB), q = r % (2 * XB);
+            return a.packed + a.a_off[s] + static_cast<int64_t>((ob * a.a_kb[s] + a.a_p0[s]) * 2 + q) * kFragBytes;
+        }
+        const int r = f - nx, ob = r / (2 * DB > 0 ? 2 * DB : 1), q = r % (2 * DB > 0 ? 2 * DB : 1);
+        return a.packed + a.dir_a_off + static_cast<int64_t>((ob * a.dir_kb + a.dir_p0) * 2 + q) * kFragBytes;
+    };
+    if constexpr (ALDS) {
+        const int nf = din_frags(a.nsrc, XB, DB, a.nc);
+        for (int i = threadIdx.x; i < nf * 64; i += kDinNT) {
+            const int f = i >> 6, l = i & 63;
+            *reinterpret_cast<u32x4*>(lds + f * kFragBytes + l * 16) =
+                *reinterpret_cast<const u32x4*>(frag_src(f) + l * 16);
+        }
+        __syncthreads();
+    }
+    auto afrag = [&](int f) -> bf16x8 {
+        if constexpr (ALDS)
+            return *reinterpret_cast<const bf16x8*>(lds + f * kFragBytes + lane * 16);
+        else
+            return *reinterpret_cast<const bf16x8*>(frag_src(f) + lane * 16);
+    };
+    const int64_t waves = static_cast<int64_t>(gridDim.x) * (kDinNT / 64);
+    for (int64_t tile = static_cast<int64_t>(blockIdx.x) * (kDinNT / 64) + (threadIdx.x >> 6); tile < a.tiles;
+         tile += waves) {
+        const int64_t tile_u = __builtin_amdgcn_readfirstlane(static_cast<int>(tile));
+        const int64_t m = tile * 32 + ml;
+        const bool valid = m < a.M;
+        if (a.g_x) {
+            f32x16 dxe[XB];
+#pragma unroll
+            for (int q = 0; q < XB; ++q) zero(dxe[q]);
+            for (int s = 0; s < a.nsrc; ++s) {
+                InBlk<PREC> b[kHB];
+#pragma unroll
+                for (int ob = 0; ob < kHB; ++ob) load_img<PREC>(a.ws + a.dz_off[s], tile_u, kHB, ob, b[ob], lane);
+#pragma unroll
+                for (int ob = 0; ob < kHB; ++ob)
+#pragma unroll
+                    for (int q = 0; q < XB; ++q) {
+                        const int f = ((s * kHB + ob) * XB + q) * 2;
+                        dxe[q] = mfma16<PREC>(afrag(f), b[ob].s[0], dxe[q]);
+                        dxe[q] = mfma16<PREC>(afrag(f + 1), b[ob].s[1], dxe[q]);
+                    }
+            }
+            const PeRev pr = pe_rev(valid ? a.x[3 * m] : 0.f, valid ? a.x[3 * m + 1] : 0.f,
+                                    valid ? a.x[3 * m + 2] : 0.f);
+            float g0 = 0.f, g1 = 0.f, g2 = 0.f;
+#pragma unroll
+            for (int kb = 0; kb < XB; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    pe_fast_bwd(pr, 32 * kb + acc_row(r, 0), 32 * kb + acc_row(r, 1), h != 0, a.L, dxe[kb][r], g0, g1,
+                                g2);
+            g0 += __shfl_xor(g0, 32);
+            g1 += __shfl_xor(g1, 32);
+            g2 += __shfl_xor(g2, 32);
+            if (valid && h == 0) {
+                a.g_x[3 * m] = g0 * a.inv_gscale;
+                a.g_x[3 * m + 1] = g1 * a.inv_gscale;
+                a.g_x[3 * m + 2] = g2 * a.inv_gscale;
+            }
+        }
+        if constexpr (DB > 0) {
+            if (a.g_d) {
+                f32x16 dd[DB];
+#pragma unroll
+                for (int q = 0; q < DB; ++q) zero(dd[q]);
+                const int f0 = 2 * a.nsrc * kHB * XB;
+                for (int ob = 0; ob < a.nc; ++ob) {
+                    InBlk<PREC> b;
+                    load_img<PREC>(a.ws + a.dz_dir_off, tile_u, a.nc, ob, b, lane);
+#pragma unroll
+                    for (int q = 0; q < DB; ++q) {
+                        const int f = f0 + (ob * DB + q) * 2;
+                        dd[q] = mfma16<PREC>(afrag(f), b.s[0], dd[q]);
+                        dd[q] = mfma16<PREC>(afrag(f + 1), b.s[1], dd[q]);
+                    }
+                }
+                const PeRev pr = pe_rev(valid ? a.d[3 * m] : 0.f, valid ? a.d[3 * m + 1] : 0.f,
+                                        valid ? a.d[3 * m + 2] : 0.f);
+                float g0 = 0.f, g1 = 0.f, g2 = 0.f;
+#pragma unroll
+                for (int kb = 0; kb < DB; ++kb)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        pe_fast_bwd(pr, 32 * kb + acc_row(r, 0), 32 * kb + acc_row(r, 1), h != 0, a.Ld, dd[kb][r], g0,
+                                    g1, g2);
+                g0 += __shfl_xor(g0, 32);
+                g1 += __shfl_xor(g1, 32);
+                g2 += __shfl_xor(g2, 32);
+                if (valid && h == 0) {
+                    a.g_d[3 * m] = g0 * a.inv_gscale;
+                    a.g_d[3 * m + 1] = g1 * a.inv_gscale;
+                    a.g_d[3 * m + 2] = g2 * a.inv_gscale;
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ dW ----
 // Workgroup = (job, chunk of tiles): 8 waves, each accumulating a 4x2-block
 // sub-grid of the job's NBz x KB output grid (<= 64 blocks).  Per tile the job's
@@ -1939,6 +2124,32 @@ int launch_bwd(const MlpPlan& p, BwdArgs& a, hipStream_t s) {
     return NR_EARG;
 }
 
+template <int PREC>
+int launch_dinput(const MlpPlan& p, const DinArgs& a, hipStream_t s) {
+    const size_t lds = static_cast<size_t>(din_frags(a.nsrc, p.XB, p.DB, a.nc)) * kFragBytes;
+    const bool alds = lds <= 160 * 1024;
+    // enough workgroups for 2 per CU (the staging is amortised over ~6 tiles per wave)
+    const dim3 grid(static_cast<unsigned>(std::min<int64_t>(ceil_div_ll(a.tiles, kDinNT / 64), 512))),
+        block(kDinNT);
+#define NR_DIN(XB_, DB_)                                                                                  \
+    if (p.XB == XB_ && p.DB == DB_) {                                                                     \
+        if (alds)                                                                                         \
+            hipLaunchKernelGGL((mlp_dinput_kernel<PREC, XB_, DB_, true>), grid, block, lds, s, a);        \
+        else                                                                                              \
+            hipLaunchKernelGGL((mlp_dinput_kernel<PREC, XB_, DB_, false>), grid, block, 0, s, a);         \
+        return check_launch("nr_mlp_backward_dx (input gradients)");                                     \
+    }
+    NR_DIN(2, 1)
+#ifndef NR_MLP_DEV
+    NR_DIN(2, 0)
+    NR_DIN(1, 1)
+    NR_DIN(1, 0)
+#endif
+#undef NR_DIN
+    set_error("nr_mlp_backward_dx: no input-gradient kernel for XB=%d DB=%d", p.XB, p.DB);
+    return NR_EARG;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2107,7 +2318,11 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     b.n_layers = p.n_layers;
     b.skips = p.skips;
     const int n = p.n_layers;
-    const bool wx = g_x != nullptr || g_d != nullptr;
+    // 16-bit: g_x / g_d come from a separate pass over the stored dz images
+    // (mlp_dinput_kernel), so the dX chain itself always runs the 8-wave variant
+    const bool want_in = g_x != nullptr || g_d != nullptr;
+    const bool split_in = want_in && p.prec != NR_PREC_FP32 && !NR_DIN_FUSED;
+    const bool wx = want_in && !split_in;
     // a skip layer's W^T chunk is [h rows | x_enc rows] and dir's is [feat rows |
     // d_enc rows]: without g_x / g_d only the first 8 row blocks are loaded
     auto add_T = [&](int l) {
@@ -2127,6 +2342,40 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     b.ws_feat = p.ws_feat;
     b.ws_dir = p.ws_dir;
     b.ws_heads = p.ws_heads;
+    if (split_in) {
+        const int rc = p.prec == NR_PREC_BF16 ? launch_bwd<NR_PREC_BF16, false>(p, b, s)
+                                              : launch_bwd<NR_PREC_FP16, false>(p, b, s);
+        if (rc != NR_OK) return rc;
+        DinArgs da;
+        std::memset(&da, 0, sizeof(da));
+        da.packed = b.packed;
+        da.ws = b.ws;
+        da.x = x;
+        da.d = d;
+        da.g_x = g_x;
+        da.g_d = g_d;
+        da.M = M;
+        da.tiles = z.tiles;
+        da.L = p.L;
+        da.Ld = p.Ld;
+        da.inv_gscale = b.inv_gscale;
+        // layer 0 reads x_enc alone; a skip layer's W^T chunk is [h (8) | x_enc (XB)]
+        for (int l = 0; l < n; ++l) {
+            if (l > 0 && !is_skip(p, l - 1)) continue;
+            da.a_off[da.nsrc] = p.lin[l].pk_bwd;
+            da.a_kb[da.nsrc] = p.lin[l].KB;
+            da.a_p0[da.nsrc] = p.lin[l].KB - p.XB;
+            da.dz_off[da.nsrc] = z.ws_off[WS_DZ0 + l];
+            da.nsrc++;
+        }
+        // dir's W^T chunk is [feat (8) | d_enc (DB)], one chunk per dz_c block
+        da.dir_a_off = p.lin[n + 1].pk_bwd;
+        da.dir_kb = p.lin[n + 1].KB;
+        da.dir_p0 = kHB;
+        da.nc = p.lin[n + 1].NB;
+        da.dz_dir_off = z.ws_off[p.ws_dir];
+        return p.prec == NR_PREC_BF16 ? launch_dinput<NR_PREC_BF16>(p, da, s) : launch_dinput<NR_PREC_FP16>(p, da, s);
+    }
     if (p.prec == NR_PREC_BF16)
         return wx ? launch_bwd<NR_PREC_BF16, true>(p, b, s) : launch_bwd<NR_PREC_BF16, false>(p, b, s);
     if (p.prec == NR_PREC_FP16)
