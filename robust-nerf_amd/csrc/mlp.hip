@@ -24,6 +24,7 @@
 // rebuilds sample-major operands with the gfx950 transpose read
 // ds_read_b64_tr_b16 (bf16) or strided ds_read_b32 (fp32).
 #include <cstring>
+#include <type_traits>
 
 #include "common.hpp"
 #include "mfma.hpp"
@@ -1167,6 +1168,8 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     }
 }
 
+#include "mlp_fwd_rbm.inc"
+
 // ----------------------------------------------------------- backward -----
 struct BwdArgs {
     float gscale, inv_gscale;  // fp16 loss scale applied to dL/d(rgb, sigma); 1 otherwise
@@ -1970,10 +1973,15 @@ __global__ void mlp_pack_kernel(PackArgs a) {
     const int h = lane >> 5, i = lane & 31;
     const int kk = bf ? 16 * sub + 8 * (el >> 2) + 4 * h + (el & 3) : acc_row(4 * sub + el, h);
     int row, col;
-    if (!bwd) {  // W: A[i][k] = W[32nb + i][col(kb, k)], chunk kb, row block nb
-        const int kb = static_cast<int>(blk / a.NB[l]), nb = static_cast<int>(blk % a.NB[l]);
+    int64_t dst_e = e;
+    if (!bwd) {  // W: A[i][k] = W[32nb + i][col(kb, k)]
+        // fp32: chunk kb, row block nb (chunk-major); 16-bit: row block nb, k block kb,
+        // then the row block's bias fragment (row-block major, mlp_fwd_rbm.inc)
+        const int kb = static_cast<int>(bf ? blk % a.KB[l] : blk / a.NB[l]);
+        const int nb = static_cast<int>(bf ? blk / a.KB[l] : blk % a.NB[l]);
         row = 32 * nb + i;
         col = pack_col(a, l, kb, kk);
+        if (bf) dst_e = ((static_cast<int64_t>(nb) * (2 * a.KB[l] + 1) + 2 * kb + sub) * 64 + lane) * epl + el;
     } else {  // W^T: A[i][k] = W[32ob + k][col(ib, i)], chunk ob, row block ib
         const int ob = static_cast<int>(blk / a.KB[l]);
         const int ib = static_cast<int>((blk % a.KB[l] + a.bwd_rot[l]) % a.KB[l]);
@@ -1983,10 +1991,39 @@ __global__ void mlp_pack_kernel(PackArgs a) {
     const float v = col >= 0 ? a.params[a.w_off[l] + static_cast<int64_t>(row) * a.in[l] + col] : 0.f;
     char* dst = a.packed + (bwd ? a.pkb[l] : a.pk[l]);
     if (bf)
-        reinterpret_cast<unsigned short*>(dst)[e] =
+        reinterpret_cast<unsigned short*>(dst)[dst_e] =
             a.prec == NR_PREC_FP16 ? __builtin_bit_cast(unsigned short, static_cast<_Float16>(v)) : bf16_bits(v);
     else
-        reinterpret_cast<float*>(dst)[e] = v;
+        reinterpret_cast<float*>(dst)[dst_e] = v;
+}
+
+// 16-bit forward images: the bias fragment that follows each row block's weights
+// (bias_frag of bias[32 nb + lane] in lanes 0..31, zeros in 32..63).
+struct PackBiasArgs {
+    const float* params;
+    char* packed;
+    int prec;
+    int n_lin;
+    int64_t pk[kMaxMfmaLayers], b_off[kMaxMfmaLayers];
+    int NB[kMaxMfmaLayers], KB[kMaxMfmaLayers], out[kMaxMfmaLayers];
+};
+
+template <int PREC>
+__device__ void pack_bias_one(const PackBiasArgs& a, int l, int nb, int lane) {
+    const int row = 32 * nb + lane;
+    const float b = (lane < 32 && row < a.out[l]) ? a.params[a.b_off[l] + row] : 0.f;
+    const bf16x8 f = bias_frag<PREC>(b);
+    char* dst = a.packed + a.pk[l] + (static_cast<int64_t>(nb) * (2 * a.KB[l] + 1) + 2 * a.KB[l]) * kFragBytes;
+    reinterpret_cast<bf16x8*>(dst)[lane] = lane < 32 ? f : bf16x8{};
+}
+
+__global__ void mlp_pack_bias_kernel(PackBiasArgs a) {
+    const int l = blockIdx.x / kMaxTrunk, nb = blockIdx.x % kMaxTrunk, lane = threadIdx.x;
+    if (l >= a.n_lin || nb >= a.NB[l]) return;
+    if (a.prec == NR_PREC_FP16)
+        pack_bias_one<NR_PREC_FP16>(a, l, nb, lane);
+    else
+        pack_bias_one<NR_PREC_BF16>(a, l, nb, lane);
 }
 
 // Vector images: element idx of a vector of NB blocks <-> feature 32*(idx>>5) + acc_row(idx&15, (idx>>4)&1).
@@ -1994,11 +2031,11 @@ struct PackVecArgs {
     const float* params;
     char* packed;
     int nv;                                   // vectors: n_lin biases, w_sigma, 3 rows of W_rgb
-    int64_t src[kMaxMfmaLayers + 4];          // float offset in params
-    int len[kMaxMfmaLayers + 4];              // valid features
-    int64_t dst[kMaxMfmaLayers + 4];          // byte offset in packed
-    int cum[kMaxMfmaLayers + 5];              // image elements (NB*32) prefix
-    int pair[kMaxMfmaLayers + 4];             // 1: pair image (PImg), 0: vector image (VImg)
+    int64_t src[kMaxMfmaLayers + 8];          // float offset in params
+    int len[kMaxMfmaLayers + 8];              // valid features
+    int64_t dst[kMaxMfmaLayers + 8];          // byte offset in packed
+    int cum[kMaxMfmaLayers + 9];              // image elements (NB*32) prefix
+    int pair[kMaxMfmaLayers + 8];             // 1: pair image (PImg), 0: vector image (VImg)
 };
 
 __global__ void mlp_pack_vec_kernel(PackVecArgs a) {
@@ -2085,6 +2122,27 @@ int launch_fwd(const MlpPlan& p, FwdArgs& a, hipStream_t s) {
     NR_FWD(1, 0)
 #endif
 #undef NR_FWD
+    set_error("nr_mlp_forward: no kernel instance for XB=%d DB=%d", p.XB, p.DB);
+    return NR_EARG;
+}
+
+template <int PREC, bool TRAIN>
+int launch_fwd_rbm(const MlpPlan& p, const RbmArgs& a, hipStream_t s) {
+    // every chunk fits a slot (checked at compile time per layer shape)
+    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, kRbmWaves))), block(kRbmWaves * 64);
+    const size_t lds = rbm_lds_bytes(p.XB);
+#define NR_FWDR(XB_, DB_)                                                                            \
+    if (p.XB == XB_ && p.DB == DB_) {                                                                \
+        hipLaunchKernelGGL((mlp_fwd_rbm_kernel<PREC, XB_, DB_, TRAIN>), grid, block, lds, s, a);      \
+        return check_launch("nr_mlp_forward");                                                       \
+    }
+    NR_FWDR(2, 1)
+#ifndef NR_MLP_DEV
+    NR_FWDR(2, 0)
+    NR_FWDR(1, 1)
+    NR_FWDR(1, 0)
+#endif
+#undef NR_FWDR
     set_error("nr_mlp_forward: no kernel instance for XB=%d DB=%d", p.XB, p.DB);
     return NR_EARG;
 }
@@ -2210,6 +2268,23 @@ int nr_mlp_pack(const NrMlpConfig* cfg, const float* params, void* packed, nr_st
     const hipStream_t s = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(mlp_pack_kernel, dim3(static_cast<unsigned>(ceil_div_ll(total, 256))), dim3(256), 0, s, a);
     NR_LAUNCH_CHECK("nr_mlp_pack");
+    if (p.prec != NR_PREC_FP32) {
+        PackBiasArgs pb;
+        std::memset(&pb, 0, sizeof(pb));
+        pb.params = params;
+        pb.packed = static_cast<char*>(packed);
+        pb.prec = p.prec;
+        pb.n_lin = p.n_lin;
+        for (int l = 0; l < p.n_lin; ++l) {
+            pb.pk[l] = p.lin[l].pk_fwd;
+            pb.b_off[l] = p.lin[l].b_off;
+            pb.NB[l] = p.lin[l].NB;
+            pb.KB[l] = p.lin[l].KB;
+            pb.out[l] = p.lin[l].out;
+        }
+        hipLaunchKernelGGL(mlp_pack_bias_kernel, dim3(p.n_lin * kMaxTrunk), dim3(64), 0, s, pb);
+        NR_LAUNCH_CHECK("nr_mlp_pack");
+    }
     PackVecArgs v;
     std::memset(&v, 0, sizeof(v));
     v.params = params;
@@ -2226,6 +2301,9 @@ int nr_mlp_pack(const NrMlpConfig* cfg, const float* params, void* packed, nr_st
     add_vec(p.sig_w, kHidden, p.vsig, kHB, 1);
     for (int c = 0; c < 3; ++c)
         add_vec(p.rgb_w + c * (kHidden / 2), kHidden / 2, p.vrgb + c * (kHidden / 2) * 4, kHB / 2, 1);
+    add_vec(p.sig_w, kHidden, p.vhead, kHB);
+    for (int c = 0; c < 3; ++c)
+        add_vec(p.rgb_w + c * (kHidden / 2), kHidden / 2, p.vhead + 1024 + c * (kHidden / 2) * 4, kHB / 2);
     hipLaunchKernelGGL(mlp_pack_vec_kernel, dim3(ceil_div(v.cum[v.nv], 256)), dim3(256), 0, s, v);
     NR_LAUNCH_CHECK("nr_mlp_pack");
     return NR_OK;
@@ -2274,10 +2352,36 @@ int nr_mlp_forward(const NrMlpConfig* cfg, const void* packed, const float* para
     a.mask_off = z.mask_off;
     a.n_mask = p.n_mask;
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    if (p.prec == NR_PREC_BF16)
-        return saved ? launch_fwd<NR_PREC_BF16, true>(p, a, s) : launch_fwd<NR_PREC_BF16, false>(p, a, s);
-    if (p.prec == NR_PREC_FP16)
-        return saved ? launch_fwd<NR_PREC_FP16, true>(p, a, s) : launch_fwd<NR_PREC_FP16, false>(p, a, s);
+    if (p.prec != NR_PREC_FP32) {
+        RbmArgs r;
+        std::memset(&r, 0, sizeof(r));
+        r.packed = a.packed;
+        r.params = params;
+        r.x = x;
+        r.d = d;
+        r.rgb = rgb;
+        r.sigma = sigma;
+        r.saved = a.saved;
+        r.M = M;
+        r.tiles = z.tiles;
+        r.L = p.L;
+        r.Ld = p.Ld;
+        r.n_layers = p.n_layers;
+        r.skips = p.skips;
+        r.base = p.lin[0].pk_fwd;
+        r.vhead = p.vhead;
+        r.sig_b = p.sig_b;
+        r.rgb_b = p.rgb_b;
+        for (int t = 0; t < p.n_saved; ++t) r.sv_off[t] = z.saved_off[t];
+        r.sv_feat = p.sv_feat;
+        r.sv_denc = p.sv_denc;
+        r.sv_hc = p.sv_hc;
+        r.mask_off = z.mask_off;
+        r.n_mask = p.n_mask;
+        if (p.prec == NR_PREC_BF16)
+            return saved ? launch_fwd_rbm<NR_PREC_BF16, true>(p, r, s) : launch_fwd_rbm<NR_PREC_BF16, false>(p, r, s);
+        return saved ? launch_fwd_rbm<NR_PREC_FP16, true>(p, r, s) : launch_fwd_rbm<NR_PREC_FP16, false>(p, r, s);
+    }
     return saved ? launch_fwd<NR_PREC_FP32, true>(p, a, s) : launch_fwd<NR_PREC_FP32, false>(p, a, s);
 }
 

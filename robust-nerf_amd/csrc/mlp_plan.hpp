@@ -92,6 +92,7 @@ struct MlpPlan {
     int64_t sig_w, sig_b, rgb_w, rgb_b;
     int64_t packed_bytes;
     int64_t vsig, vrgb;               // byte offsets of the w_sigma / W_rgb vector images
+    int64_t vhead;                    // 16-bit forward: w_sigma then the 3 W_rgb rows as vector images (3 KB)
     int esize;                        // bytes per saved/workspace element (2 bf16, 4 fp32)
     int fpb;                          // 1-KB fragments per 32x32 block (2 bf16, 4 fp32)
     // saved tensors
