@@ -25,6 +25,7 @@
 // ds_read_b64_tr_b16 (bf16) or strided ds_read_b32 (fp32).
 #include <cstring>
 #include <type_traits>
+#include <utility>
 
 #include "common.hpp"
 #include "mfma.hpp"
