@@ -530,6 +530,9 @@ struct Ring {
 #ifndef NR_SINK_BWD
 #define NR_SINK_BWD 0  // 1: store each dz while the next stream consumes it (measured slower: 1.50 vs 1.35 ms)
 #endif
+#ifndef NR_BWD_RBM
+#define NR_BWD_RBM 1  // 16-bit dX chain: 1 row-block major (mlp_bwd_rbm.inc), 0 chunk-major mlp_bwd_kernel
+#endif
 #ifndef NR_DIN_FUSED
 #define NR_DIN_FUSED 0  // 1: 16-bit g_x / g_d through the 4-wave input-gradient dX variant (A/B)
 #endif
@@ -1170,6 +1173,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
 }
 
 #include "mlp_fwd_rbm.inc"
+#include "mlp_bwd_rbm.inc"
 
 // ----------------------------------------------------------- backward -----
 struct BwdArgs {
@@ -1998,6 +2002,38 @@ __global__ void mlp_pack_kernel(PackArgs a) {
         reinterpret_cast<float*>(dst)[dst_e] = v;
 }
 
+// 16-bit dX-chain images (pk_bwdr): for layers l >= 1, A[i][k] = W[32 ob + k][hcol0 +
+// 32 ib + i] with ib the hidden input block (row block), ob the output block (k
+// block), row-block major: e = ((ib * NB + ob) * 2 + frag) * 512 + lane * 8 + el.
+struct PackBwdrArgs {
+    const float* params;
+    char* packed;
+    int prec;
+    int l0, n_lin;                         // layers l0 .. n_lin-1
+    int64_t w_off[kMaxMfmaLayers], pk[kMaxMfmaLayers];
+    int in[kMaxMfmaLayers], NB[kMaxMfmaLayers], out[kMaxMfmaLayers], hcol0[kMaxMfmaLayers];
+    int64_t cum[kMaxMfmaLayers + 1];       // element prefix over layers l0..
+};
+
+__global__ void mlp_pack_bwdr_kernel(PackBwdrArgs a) {
+    const int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (g >= a.cum[a.n_lin]) return;
+    int l = a.l0;
+    while (g >= a.cum[l + 1]) ++l;
+    const int64_t e = g - a.cum[l];
+    const int el = static_cast<int>(e % 8), lane = static_cast<int>((e / 8) % 64);
+    const int64_t frag = e / 512;
+    const int sub = static_cast<int>(frag % 2);
+    const int64_t blk = frag / 2;
+    const int ob = static_cast<int>(blk % a.NB[l]), ib = static_cast<int>(blk / a.NB[l]);
+    const int h = lane >> 5, i = lane & 31;
+    const int kk = 16 * sub + 8 * (el >> 2) + 4 * h + (el & 3);
+    const int row = 32 * ob + kk, col = a.hcol0[l] + 32 * ib + i;
+    const float v = row < a.out[l] ? a.params[a.w_off[l] + static_cast<int64_t>(row) * a.in[l] + col] : 0.f;
+    unsigned short* dst = reinterpret_cast<unsigned short*>(a.packed + a.pk[l]);
+    dst[e] = a.prec == NR_PREC_FP16 ? __builtin_bit_cast(unsigned short, static_cast<_Float16>(v)) : bf16_bits(v);
+}
+
 // 16-bit forward images: the bias fragment that follows each row block's weights
 // (bias_frag of bias[32 nb + lane] in lanes 0..31, zeros in 32..63).
 struct PackBiasArgs {
@@ -2148,6 +2184,18 @@ int launch_fwd_rbm(const MlpPlan& p, const RbmArgs& a, hipStream_t s) {
     return NR_EARG;
 }
 
+template <int PREC>
+int launch_bwd_rbm(const MlpPlan& p, const BwdrArgs& a, hipStream_t s) {
+    const size_t lds = bwdr_lds_bytes(p.n_mask);
+    if (lds > 160 * 1024) {
+        set_error("nr_mlp_backward_dx: %zu bytes of LDS exceed 160 KiB", lds);
+        return NR_EARG;
+    }
+    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, kRbmWaves))), block(kRbmWaves * 64);
+    hipLaunchKernelGGL((mlp_bwd_rbm_kernel<PREC>), grid, block, lds, s, a);
+    return check_launch("nr_mlp_backward_dx");
+}
+
 template <int PREC, bool WX>
 int launch_bwd(const MlpPlan& p, BwdArgs& a, hipStream_t s) {
     // the input-gradient variant also carries d x_enc through the trunk: 4 waves, 512 registers
@@ -2285,6 +2333,31 @@ int nr_mlp_pack(const NrMlpConfig* cfg, const float* params, void* packed, nr_st
         }
         hipLaunchKernelGGL(mlp_pack_bias_kernel, dim3(p.n_lin * kMaxTrunk), dim3(64), 0, s, pb);
         NR_LAUNCH_CHECK("nr_mlp_pack");
+        if (p.n_lin > 1) {
+            PackBwdrArgs pr;
+            std::memset(&pr, 0, sizeof(pr));
+            pr.params = params;
+            pr.packed = static_cast<char*>(packed);
+            pr.prec = p.prec;
+            pr.l0 = 1;
+            pr.n_lin = p.n_lin;
+            pr.cum[1] = 0;
+            for (int l = 1; l < p.n_lin; ++l) {
+                const LinearDesc& d = p.lin[l];
+                pr.w_off[l] = d.w_off;
+                pr.pk[l] = d.pk_bwdr;
+                pr.in[l] = d.in;
+                pr.NB[l] = d.NB;
+                pr.out[l] = d.out;
+                // the hidden input columns: after x_enc in a skip layer (cat([x_enc, h])), first otherwise
+                pr.hcol0[l] = (l < p.n_layers && is_skip(p, l - 1)) ? p.pos_dim : 0;
+                pr.cum[l + 1] = pr.cum[l] + static_cast<int64_t>(kHB) * d.NB * 1024;
+            }
+            const int64_t tot = pr.cum[p.n_lin];
+            hipLaunchKernelGGL(mlp_pack_bwdr_kernel, dim3(static_cast<unsigned>(ceil_div_ll(tot, 256))), dim3(256), 0,
+                               s, pr);
+            NR_LAUNCH_CHECK("nr_mlp_pack");
+        }
     }
     PackVecArgs v;
     std::memset(&v, 0, sizeof(v));
@@ -2447,9 +2520,39 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     b.ws_feat = p.ws_feat;
     b.ws_dir = p.ws_dir;
     b.ws_heads = p.ws_heads;
+    // 16-bit dX chain: row-block major (mlp_bwd_rbm.inc)
+    auto chain16 = [&]() -> int {
+#if NR_BWD_RBM
+        BwdrArgs r;
+        std::memset(&r, 0, sizeof(r));
+        r.gscale = b.gscale;
+        r.packed = b.packed;
+        r.rgb = rgb;
+        r.sigma = sigma;
+        r.g_rgb = g_rgb;
+        r.g_sigma = g_sigma;
+        r.saved = b.saved;
+        r.ws = b.ws;
+        r.M = M;
+        r.tiles = z.tiles;
+        r.n_layers = n;
+        r.base = p.lin[n + 1].pk_bwdr;
+        r.vrgb = p.vrgb;
+        r.vhead = p.vhead;
+        r.mask_off = z.mask_off;
+        r.n_mask = p.n_mask;
+        for (int t = 0; t < p.n_ws; ++t) r.ws_off[t] = z.ws_off[t];
+        r.ws_feat = p.ws_feat;
+        r.ws_dir = p.ws_dir;
+        r.ws_heads = p.ws_heads;
+        return p.prec == NR_PREC_BF16 ? launch_bwd_rbm<NR_PREC_BF16>(p, r, s) : launch_bwd_rbm<NR_PREC_FP16>(p, r, s);
+#else
+        return p.prec == NR_PREC_BF16 ? launch_bwd<NR_PREC_BF16, false>(p, b, s)
+                                      : launch_bwd<NR_PREC_FP16, false>(p, b, s);
+#endif
+    };
     if (split_in) {
-        const int rc = p.prec == NR_PREC_BF16 ? launch_bwd<NR_PREC_BF16, false>(p, b, s)
-                                              : launch_bwd<NR_PREC_FP16, false>(p, b, s);
+        const int rc = chain16();
         if (rc != NR_OK) return rc;
         DinArgs da;
         std::memset(&da, 0, sizeof(da));
@@ -2481,10 +2584,9 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
         da.dz_dir_off = z.ws_off[p.ws_dir];
         return p.prec == NR_PREC_BF16 ? launch_dinput<NR_PREC_BF16>(p, da, s) : launch_dinput<NR_PREC_FP16>(p, da, s);
     }
-    if (p.prec == NR_PREC_BF16)
-        return wx ? launch_bwd<NR_PREC_BF16, true>(p, b, s) : launch_bwd<NR_PREC_BF16, false>(p, b, s);
-    if (p.prec == NR_PREC_FP16)
-        return wx ? launch_bwd<NR_PREC_FP16, true>(p, b, s) : launch_bwd<NR_PREC_FP16, false>(p, b, s);
+    if (p.prec != NR_PREC_FP32 && !wx) return chain16();
+    if (p.prec == NR_PREC_BF16) return launch_bwd<NR_PREC_BF16, true>(p, b, s);
+    if (p.prec == NR_PREC_FP16) return launch_bwd<NR_PREC_FP16, true>(p, b, s);
     return wx ? launch_bwd<NR_PREC_FP32, true>(p, b, s) : launch_bwd<NR_PREC_FP32, false>(p, b, s);
 }
 

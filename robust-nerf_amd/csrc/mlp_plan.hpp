@@ -44,6 +44,7 @@ struct LinearDesc {
     int nseg;
     Seg seg[kMaxSeg];
     int64_t pk_fwd, pk_bwd;  // byte offsets of the W / W^T fragment images
+    int64_t pk_bwdr;         // 16-bit: row-block-major W^T image of the h (feat) input rows (dX chain)
     int64_t vb;              // byte offset of the bias vector image (accumulator order)
 };
 
