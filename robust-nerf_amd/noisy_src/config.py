@@ -9,9 +9,11 @@ only defaulted fields:
 * ``ModelConfig.precision`` — ``"fp32"`` (exact fp32 MFMA, the parity mode),
   ``"bf16"`` (bf16 MFMA operands, fp32 accumulation and fp32 master weights) or
   ``"fp16"`` (BASELINE cfg #5: fp16 operands, fp32 accumulation, backward on dz
-  scaled by 2^14);
-* ``TrainConfig.world_size`` / ``TrainConfig.global_batch`` — ray-batch data
-  parallelism over RCCL (one process per GPU).
+  scaled by 2^14).
+
+Data parallelism adds no config field: under ``torchrun`` the entry points read
+RANK/WORLD_SIZE from the environment and slice the shared-seed global batch
+(``DataConfig.batch_size`` rays) per rank.
 """
 
 from dataclasses import dataclass, field

@@ -27,6 +27,8 @@ ROOT = Path(__file__).resolve().parents[1]
 
 # fused-MLP grid size (workgroups x threads) -> samples M, per kernel family
 FAMILIES = {"mlp_fwd_kernel": "nr_mlp_forward", "mlp_bwd_kernel": "nr_mlp_backward_dx",
+            "mlp_fwd_rbm_kernel": "nr_mlp_forward", "mlp_bwd_rbm_kernel": "nr_mlp_backward_dx",
+            "mlp_dinput_kernel": "nr_mlp_backward_dx (input grads)",
             "mlp_dw_kernel": "nr_mlp_backward_dw", "mlp_dw_reduce_kernel": "nr_mlp_backward_reduce"}
 
 
@@ -44,9 +46,9 @@ def sample_count(name: str, grid: int, last_M: int) -> int:
     """M of a fused-MLP launch: the forward/backward kernels run one 32-sample tile per
     wave; dW and its reduction follow the backward launch of the same M in the stream."""
     fam = short(name)
-    if fam in ("mlp_fwd_kernel", "mlp_bwd_kernel"):
+    if fam in ("mlp_fwd_kernel", "mlp_bwd_kernel", "mlp_fwd_rbm_kernel", "mlp_bwd_rbm_kernel"):
         return grid // 64 * 32
-    if fam in ("mlp_dw_kernel", "mlp_dw_reduce_kernel"):
+    if fam in ("mlp_dw_kernel", "mlp_dw_reduce_kernel", "mlp_dinput_kernel"):
         return last_M
     return 0
 
@@ -97,7 +99,9 @@ def main(out_dir: str, tag: str) -> None:
                      "bytes_per_launch": 2.0 * fetch + write, "launches": len(c["FETCH_SIZE"])})
     out = {"source": f"profiles/{tag}: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
                      "python bench.py --steps 2 --warmup 1; traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (median)",
-           "kernels": recs}
+           "kernels": recs,
+           # each (kernel, M) launches once per training step: the step's MLP HBM bytes
+           "per_step_mlp_bytes": sum(r["bytes_per_launch"] for r in recs)}
     (ROOT / "profiles" / "traffic.json").write_text(json.dumps(out, indent=1))
     print(json.dumps(out, indent=1))
 
