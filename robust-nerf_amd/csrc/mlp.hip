@@ -1596,17 +1596,30 @@ __global__ __launch_bounds__(kDinNT) void mlp_dinput_kernel(DinArgs a) {
 }
 
 // ------------------------------------------------------------------ dW ----
-// Workgroup = (job, chunk of tiles): 8 waves, each accumulating a 4x2-block
-// sub-grid of the job's NBz x KB output grid (<= 64 blocks).  Per tile the job's
-// dz and input blocks are staged into LDS by LDS-DMA (double buffered, 1-KB wave
-// pieces) and the sample-major MFMA operands are rebuilt from the B-operand
-// images.  Output slab per chunk: [dz row][input col | bias] fp32.
+// Workgroup = (job, chunk of tiles): 8 waves, each accumulating its planned share
+// (DwWave: up to 5x2 blocks) of the job's NBz x KB output grid.  Per tile the
+// job's dz and input blocks (every tensor once: h_{n-1} feeds the feature layer
+// and the sigma head in one job) are staged into LDS by LDS-DMA (a 4-stage ring of
+// 1-KB wave pieces) and the sample-major MFMA operands are rebuilt from the
+// B-operand images.  Bias partials are v_dot2 sums of the dz operands.  Output
+// slab per chunk: [dz row][input col | bias] fp32.  The kernel runs at its staging
+// ceiling: the same staging with the MFMAs compiled out (NR_DW_NOCOMPUTE) is
+// within 1 % of it.
 #ifndef NR_DW_NSTAGE
 #define NR_DW_NSTAGE 4  // LDS staging ring depth of the dW kernel (tiles)
 #endif
+#ifndef NR_DW_ONESHAPE
+#define NR_DW_ONESHAPE 0  // A/B only: every 16-bit wave share runs as 5x2
+#endif
+#ifndef NR_DW_NOBIAS
+#define NR_DW_NOBIAS 0  // A/B only: skip the bias sums (wrong bias gradients)
+#endif
+#ifndef NR_DW_NOCOMPUTE
+#define NR_DW_NOCOMPUTE 0  // A/B only: stage the tiles, skip the MFMAs (staging ceiling)
+#endif
 constexpr int kDwThreads = 512;
 constexpr int kDwWaves = kDwThreads / 64;
-constexpr int kDwP = 4, kDwQ = 2;  // blocks per wave: dz rows x input cols
+static_assert(kDwWaves == kDwMaxWaves, "dW wave shares are planned for 8-wave workgroups");
 
 struct DwArgs {
     float* slabs;
@@ -1615,11 +1628,18 @@ struct DwArgs {
     int tiles_per_chunk, chunks;
     int stage_bytes, nstage;
     int64_t slab_floats_per_chunk;
-    int job_NBz[kMaxJobs], job_KB[kMaxJobs], job_nbg[kMaxJobs], job_waves[kMaxJobs], job_nseg[kMaxJobs];
+    int job_NBz[kMaxJobs], job_KB[kMaxJobs], job_nseg[kMaxJobs];
     int64_t job_slab[kMaxJobs];
     const char* seg_ptr[kMaxJobs][2 * kMaxJobSeg];  // tensor region: dz segments, then inputs
     int seg_blocks[kMaxJobs][2 * kMaxJobSeg];  // int: scalar-loadable
+    // wave share (DwWave) packed: row0 | np << 6 | col0 << 9 | nq << 15 | bias << 17; 0 = idle
+    int job_wave[kMaxJobs][kDwWaves];
 };
+static_assert(sizeof(DwArgs) <= 4096, "dW kernel arguments exceed 4 KiB");
+
+__host__ __device__ constexpr int dw_wave_pack(int row0, int np, int col0, int nq, int bias) {
+    return row0 | np << 6 | col0 << 9 | nq << 15 | bias << 17;
+}
 
 // Block-local feature of dW operand row/col index r: r = 16h + i <-> accumulator
 // register i of lane half h in the B-operand image.
@@ -1662,21 +1682,41 @@ __device__ __forceinline__ uint32_t dw_tr_off(int ks, int half, int lane) {
     return static_cast<uint32_t>(s * kFragBytes + dw_slot(L, s) * 16 + 8 * (p & 1));
 }
 
+// acc + the four 16-bit values of a transpose read (bias partial sums): two
+// v_dot2c_f32_{bf16,f16} against (1, 1), fp32 accumulation
+template <int PREC>
+__device__ __forceinline__ float dw_acc4(uint64_t v, float acc) {
+    const unsigned w0 = static_cast<unsigned>(v), w1 = static_cast<unsigned>(v >> 32);
+    if constexpr (PREC == NR_PREC_FP16) {
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        const h2 one = __builtin_bit_cast(h2, 0x3c003c00u);
+        acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, w0), one, acc, false);
+        return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, w1), one, acc, false);
+    } else {
+        typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+        const b2 one = __builtin_bit_cast(b2, 0x3f803f80u);
+        acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2, w0), one, acc, false);
+        return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2, w1), one, acc, false);
+    }
+}
+
 template <int PREC>
 __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar staging loop
 #if NR_DW_CHUNK_MAJOR
-    // chunk-major: every job of a chunk runs at about the same time, so an input two
-    // jobs share (h_{n-1}: feature and heads jobs) is re-read from L2/MALL, not HBM
+    // chunk-major: every job of a chunk runs at about the same time (an input two
+    // jobs share, x_enc of the x-jobs beyond the first, is re-read from L2/MALL)
     const int j = blockIdx.x % a.njobs, chunk = blockIdx.x / a.njobs;
 #else
     const int j = blockIdx.x / a.chunks, chunk = blockIdx.x % a.chunks;
 #endif
     const int NBz = a.job_NBz[j], KB = a.job_KB[j];
-    const bool active = wv < a.job_waves[j];
-    const int nbg = active ? wv % a.job_nbg[j] : 0, kbg = active ? wv / a.job_nbg[j] : 0;
+    const int winfo = a.job_wave[j][wv];
+    const int row0 = winfo & 63, np = (winfo >> 6) & 7, col0 = (winfo >> 9) & 63, nq = (winfo >> 15) & 3;
+    const bool active = np > 0;
+    const bool do_bias = active && ((winfo >> 17) & 1);
     const int64_t t0 = static_cast<int64_t>(chunk) * a.tiles_per_chunk;
     int64_t t1 = t0 + a.tiles_per_chunk;
     if (t1 > a.tiles) t1 = a.tiles;
@@ -1740,82 +1780,89 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
         }
     };
 
-    f32x16 acc[kDwP][kDwQ];
-#pragma unroll
-    for (int p = 0; p < kDwP; ++p)
-#pragma unroll
-        for (int q = 0; q < kDwQ; ++q) zero(acc[p][q]);
-    float bsum[kDwP] = {0.f, 0.f, 0.f, 0.f};  // fp32 images
-    f32x16 accb[kDwP];                        // bf16 images: D[row][*] = sum of dz[row]
-    const bf16x8 ones = ones16<PREC>();
-#pragma unroll
-    for (int p = 0; p < kDwP; ++p) zero(accb[p]);
-    bool nval[kDwP], kval[kDwQ];
-#pragma unroll
-    for (int p = 0; p < kDwP; ++p) nval[p] = active && kDwP * nbg + p < NBz;
-#pragma unroll
-    for (int q = 0; q < kDwQ; ++q) kval[q] = active && kDwQ * kbg + q < KB;
-    const bool do_bias = active && kbg == 0;
-
     uint32_t trof[2][2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) trof[ks][hf] = dw_tr_off(ks, hf, lane);
-
     const int NS = a.nstage;
-    for (int k = 0; k < NS - 1; ++k)
-        if (t0 + k < t1) stage(k);
-    int bcur = 0, bnext = NS - 1;  // stage of tile t, stage tile t+NS-1 goes to
-    for (int64_t t = t0; t < t1; ++t) {
-        // stages t+1 .. t+NS-2 may stay in flight
-        int64_t ahead = t1 - 1 - t;
-        if (ahead > NS - 2) ahead = NS - 2;
-        wait_pieces(per_wave * static_cast<int>(ahead));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (t + NS - 1 < t1) stage(bnext);
-        bnext = bnext + 1 == NS ? 0 : bnext + 1;
-        const char* buf = lds + bcur * a.stage_bytes;
-        bcur = bcur + 1 == NS ? 0 : bcur + 1;
-        if (k16<PREC> || active) {
+    float* slab = a.slabs + static_cast<int64_t>(chunk) * a.slab_floats_per_chunk + a.job_slab[j];
+    const int ld = KB * 32 + 1;
+    const int hl = lane >> 5, ml = lane & 31;
+
+    // The tile loop and the slab write for a compile-time share shape NP x NQ (16-bit:
+    // the share's np x nq blocks run as the next compiled shape up, the extra blocks
+    // accumulate garbage that is never written; fp32: kDwMaxP x kDwMaxQ with runtime
+    // validity).  Each shape's accumulators live only inside its own instantiation.
+    auto run = [&](auto npc, auto nqc) {
+        constexpr int NP = decltype(npc)::value, NQ = decltype(nqc)::value;
+        f32x16 acc[NP][NQ];
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) zero(acc[p][q]);
+        float bsum[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) bsum[p] = 0.f;
+        bool nval[NP], kval[NQ];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) nval[p] = p < np;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) kval[q] = q < nq;
+
+        for (int k = 0; k < NS - 1; ++k)
+            if (t0 + k < t1) stage(k);
+        int bcur = 0, bnext = NS - 1;  // stage of tile t, stage tile t+NS-1 goes to
+        for (int64_t t = t0; t < t1; ++t) {
+            // stages t+1 .. t+NS-2 may stay in flight
+            int64_t ahead = t1 - 1 - t;
+            if (ahead > NS - 2) ahead = NS - 2;
+            wait_pieces(per_wave * static_cast<int>(ahead));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (t + NS - 1 < t1) stage(bnext);
+            bnext = bnext + 1 == NS ? 0 : bnext + 1;
+            const char* buf = lds + bcur * a.stage_bytes;
+            bcur = bcur + 1 == NS ? 0 : bcur + 1;
+            if (NR_DW_NOCOMPUTE || !active) continue;
             if constexpr (k16<PREC>) {
-                const uint32_t bufA = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf)) + kDwP * nbg * BLK;
-                const uint32_t bufB = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf)) +
-                                      (NBz + kDwQ * kbg) * BLK;
+                const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf));
+                const uint32_t bufA = base + row0 * BLK, bufB = base + (NBz + col0) * BLK;
 #pragma unroll
                 for (int ks = 0; ks < 2; ++ks) {
-                    uint64_t ra[kDwP][2], rb[kDwQ][2];
+                    uint64_t ra[NP][2], rb[NQ][2];
 #pragma unroll
                     for (int hf = 0; hf < 2; ++hf) {
                         const uint32_t oa = bufA + trof[ks][hf], ob = bufB + trof[ks][hf];
-                        tr16<0 * BLK>(ra[0][hf], oa);
-                        tr16<1 * BLK>(ra[1][hf], oa);
-                        tr16<2 * BLK>(ra[2][hf], oa);
-                        tr16<3 * BLK>(ra[3][hf], oa);
-                        tr16<0 * BLK>(rb[0][hf], ob);
-                        tr16<1 * BLK>(rb[1][hf], ob);
+                        rbm_static_for<NP>(
+                            [&](auto pp) { tr16<decltype(pp)::value * BLK>(ra[decltype(pp)::value][hf], oa); });
+                        rbm_static_for<NQ>(
+                            [&](auto qq) { tr16<decltype(qq)::value * BLK>(rb[decltype(qq)::value][hf], ob); });
                     }
-                    asm volatile("s_waitcnt lgkmcnt(0)"
-                                 : "+v"(ra[0][0]), "+v"(ra[0][1]), "+v"(ra[1][0]), "+v"(ra[1][1]), "+v"(ra[2][0]),
-                                   "+v"(ra[2][1]), "+v"(ra[3][0]), "+v"(ra[3][1]), "+v"(rb[0][0]), "+v"(rb[0][1]),
-                                   "+v"(rb[1][0]), "+v"(rb[1][1]));
-                    bf16x8 A[kDwP], Bm[kDwQ];
+                    // the wait publishes the transpose reads: tie every destination to it
+                    // (volatile asm keeps its order) so no use is scheduled above it
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-                    for (int p = 0; p < kDwP; ++p) A[p] = tr_pair(ra[p][0], ra[p][1]);
+                    for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
-                    for (int q = 0; q < kDwQ; ++q) Bm[q] = tr_pair(rb[q][0], rb[q][1]);
+                        for (int p = 0; p < NP; ++p) asm volatile("" : "+v"(ra[p][hf]));
 #pragma unroll
-                    // branch-free: blocks outside the job (and idle waves) accumulate
-                    // garbage that is never written (LDS reads past the image are in range
-                    // or return 0); per-MFMA validity branches made this loop SALU-bound
-                    for (int p = 0; p < kDwP; ++p)
+                        for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(rb[q][hf]));
+                    }
+                    bf16x8 A[NP], Bm[NQ];
 #pragma unroll
-                        for (int q = 0; q < kDwQ; ++q) acc[p][q] = mfma16<PREC>(A[p], Bm[q], acc[p][q]);
-                    // bias gradient = dz summed over samples: an MFMA against ones
-                    if (do_bias)
+                    for (int p = 0; p < NP; ++p) A[p] = tr_pair(ra[p][0], ra[p][1]);
 #pragma unroll
-                        for (int p = 0; p < kDwP; ++p) accb[p] = mfma16<PREC>(A[p], ones, accb[p]);
+                    for (int q = 0; q < NQ; ++q) Bm[q] = tr_pair(rb[q][0], rb[q][1]);
+                    // branch-free: per-MFMA validity branches made this loop SALU-bound
+#pragma unroll
+                    for (int p = 0; p < NP; ++p)
+#pragma unroll
+                        for (int q = 0; q < NQ; ++q) acc[p][q] = mfma16<PREC>(A[p], Bm[q], acc[p][q]);
+                    // bias gradient = dz summed over samples: lane-local fp32 partials
+                    if (do_bias && !NR_DW_NOBIAS)
+#pragma unroll
+                        for (int p = 0; p < NP; ++p) bsum[p] = dw_acc4<PREC>(ra[p][1], dw_acc4<PREC>(ra[p][0], bsum[p]));
                 }
             } else {
                 // fp32 image [tq][L][4]: operand row r <-> (hh = r>>4, reg i = r&15 -> frag i>>2, elem i&3)
@@ -1825,58 +1872,59 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
 #pragma unroll 4
                 for (int ss = 0; ss < 16; ++ss) {
                     const int m = 2 * ss + kk;
-                    float A[kDwP], Bv[kDwQ];
+                    float A[NP], Bv[NQ];
 #pragma unroll
-                    for (int p = 0; p < kDwP; ++p)
-                        A[p] = nval[p] ? *reinterpret_cast<const float*>(buf + (kDwP * nbg + p) * BLK + off + m * 16)
-                                       : 0.f;
+                    for (int p = 0; p < NP; ++p)
+                        A[p] = nval[p] ? *reinterpret_cast<const float*>(buf + (row0 + p) * BLK + off + m * 16) : 0.f;
 #pragma unroll
-                    for (int q = 0; q < kDwQ; ++q)
-                        Bv[q] = kval[q] ? *reinterpret_cast<const float*>(buf + (NBz + kDwQ * kbg + q) * BLK + off +
-                                                                          m * 16)
+                    for (int q = 0; q < NQ; ++q)
+                        Bv[q] = kval[q] ? *reinterpret_cast<const float*>(buf + (NBz + col0 + q) * BLK + off + m * 16)
                                         : 0.f;
 #pragma unroll
-                    for (int p = 0; p < kDwP; ++p) {
+                    for (int p = 0; p < NP; ++p) {
                         if (!nval[p]) continue;
                         if (do_bias) bsum[p] += A[p];
 #pragma unroll
-                        for (int q = 0; q < kDwQ; ++q)
+                        for (int q = 0; q < NQ; ++q)
                             if (kval[q]) acc[p][q] = mfma_f32(A[p], Bv[q], acc[p][q]);
                     }
                 }
             }
         }
-    }
-    if (!active) return;
-    float* slab = a.slabs + static_cast<int64_t>(chunk) * a.slab_floats_per_chunk + a.job_slab[j];
-    const int ld = KB * 32 + 1;
-    const int hl = lane >> 5, ml = lane & 31;
+        if (!active) return;
 #pragma unroll
-    for (int p = 0; p < kDwP; ++p) {
-        if (!nval[p]) continue;
+        for (int p = 0; p < NP; ++p) {
+            if (!nval[p]) continue;
 #pragma unroll
-        for (int q = 0; q < kDwQ; ++q) {
-            if (!kval[q]) continue;
+            for (int q = 0; q < NQ; ++q) {
+                if (!kval[q]) continue;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = 32 * (kDwP * nbg + p) + dw_feat(acc_row(r, hl));
-                const int col = 32 * (kDwQ * kbg + q) + dw_feat(ml);
-                slab[static_cast<int64_t>(row) * ld + col] = acc[p][q][r];
+                for (int r = 0; r < 16; ++r) {
+                    const int row = 32 * (row0 + p) + dw_feat(acc_row(r, hl));
+                    const int col = 32 * (col0 + q) + dw_feat(ml);
+                    slab[static_cast<int64_t>(row) * ld + col] = acc[p][q][r];
+                }
             }
-        }
-        if (do_bias) {
-            if constexpr (k16<PREC>) {
-                // every column of accb holds the row sums: lanes 0 and 32 (column 0) write them
-                if (ml == 0)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        slab[static_cast<int64_t>(32 * (kDwP * nbg + p) + dw_feat(acc_row(r, hl))) * ld + KB * 32] =
-                            accb[p][r];
-            } else {
+            if (do_bias) {
+                // lanes l and l+32 summed the two sample halves of operand row l & 31
                 const float tot = bsum[p] + __shfl_xor(bsum[p], 32);
-                if (hl == 0) slab[static_cast<int64_t>(32 * (kDwP * nbg + p) + dw_feat(ml)) * ld + KB * 32] = tot;
+                if (hl == 0) slab[static_cast<int64_t>(32 * (row0 + p) + dw_feat(ml)) * ld + KB * 32] = tot;
             }
         }
+    };
+    using std::integral_constant;
+    if constexpr (k16<PREC> && !NR_DW_ONESHAPE) {
+        // compiled shares: 1x2, 4x1, 4x2, 5x2 (a smaller share runs the next one up)
+        if (np <= 1)
+            run(integral_constant<int, 1>{}, integral_constant<int, 2>{});
+        else if (np <= 4 && nq <= 1)
+            run(integral_constant<int, 4>{}, integral_constant<int, 1>{});
+        else if (np <= 4)
+            run(integral_constant<int, 4>{}, integral_constant<int, 2>{});
+        else
+            run(integral_constant<int, kDwMaxP>{}, integral_constant<int, kDwMaxQ>{});
+    } else {
+        run(integral_constant<int, kDwMaxP>{}, integral_constant<int, kDwMaxQ>{});
     }
 }
 
@@ -2614,10 +2662,18 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
         const DwJob& jb = p.job[j];
         w.job_NBz[j] = jb.NBz;
         w.job_KB[j] = jb.KB;
-        w.job_nbg[j] = ceil_div(jb.NBz, kDwP);
-        w.job_waves[j] = w.job_nbg[j] * ceil_div(jb.KB, kDwQ);
-        NR_REQUIRE(w.job_waves[j] <= kDwWaves, "nr_mlp_backward_dw: job %d grid %dx%d exceeds the workgroup", j,
-                   jb.NBz, jb.KB);
+        for (int v = 0; v < kDwWaves; ++v) {
+            if (v >= jb.nwaves) {
+                w.job_wave[j][v] = 0;
+                continue;
+            }
+            const DwWave& sh = jb.w[v];
+            NR_REQUIRE(sh.np >= 1 && sh.np <= kDwMaxP && sh.nq >= 1 && sh.nq <= kDwMaxQ && sh.row0 >= 0 &&
+                           sh.row0 + sh.np <= jb.NBz && sh.col0 >= 0 && sh.col0 + sh.nq <= jb.KB && jb.NBz < 64 &&
+                           jb.KB < 64,
+                       "nr_mlp_backward_dw: job %d wave %d share out of its %dx%d grid", j, v, jb.NBz, jb.KB);
+            w.job_wave[j][v] = dw_wave_pack(sh.row0, sh.np, sh.col0, sh.nq, sh.bias);
+        }
         int ns = 0;
         for (int q = 0; q < jb.ndz; ++q, ++ns) {
             w.seg_ptr[j][ns] = (jb.dz[q].is_ws ? ws : sv) + (jb.dz[q].is_ws ? z.ws_off : z.saved_off)[jb.dz[q].tensor];

@@ -54,15 +54,27 @@ struct DwSeg {
     int is_ws, tensor, blocks;
 };
 
-// A dW job: the products dz^T . in of every (dz tensor, input tensor) pair it
-// lists, for the tiles of one chunk: an NBz x KB grid of 32x32 blocks (at most
-// 64 blocks = 8 waves x 4x2).  Output slab per chunk: (NBz*32) x (KB*32 + 1)
-// floats, the last column holding the bias partial sums of the dz rows.
+// One wave's share of a dW job: dz row blocks [row0, row0+np) x input column
+// blocks [col0, col0+nq) (np <= kDwMaxP, nq <= kDwMaxQ), plus the bias partial
+// sums of those dz rows when bias != 0.
+constexpr int kDwMaxWaves = 8;
+constexpr int kDwMaxP = 5, kDwMaxQ = 2;
+struct DwWave {
+    int row0, np, col0, nq, bias;
+};
+
+// A dW job: products dz^T . in over the tiles of one chunk, for the 32x32 blocks
+// its waves list, inside an NBz x KB grid (dz segments stacked as rows, input
+// segments as columns; every tensor is staged once per tile).  Output slab per
+// chunk: (NBz*32) x (KB*32 + 1) floats, the last column holding the bias partial
+// sums of the dz rows; blocks no wave lists are never written or read.
 struct DwJob {
     int ndz, nin;
     DwSeg dz[kMaxJobSeg], in[kMaxJobSeg];
     int NBz, KB;
     int64_t slab_off;  // float offset of this job's slab inside one chunk's slab set
+    int nwaves;
+    DwWave w[kDwMaxWaves];
 };
 
 // Saved tensor ids (training forward) and workspace tensor ids (backward).
