@@ -1945,16 +1945,18 @@ struct ReduceArgs {
 };
 
 __global__ void mlp_dw_reduce_kernel(ReduceArgs a) {
-    const int64_t pidx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    // 32-bit index math: a parameter index and its offset inside a range fit easily
+    // (64-bit division made the index walk dominate this memory-bound kernel)
+    const int pidx = static_cast<int>(blockIdx.x) * static_cast<int>(blockDim.x) + static_cast<int>(threadIdx.x);
     if (pidx >= a.param_count) return;
-    int job = -1;
-    int64_t row = 0, col = 0;
+    int job = -1, row = 0, col = 0;
     for (int k = 0; k < a.n_red && job < 0; ++k) {
-        const int64_t wsz = static_cast<int64_t>(a.rows[k]) * a.in[k];
-        if (pidx >= a.w_off[k] && pidx < a.w_off[k] + wsz) {
-            const int64_t e = pidx - a.w_off[k];
-            const int r = static_cast<int>(e / a.in[k]);
-            const int c = static_cast<int>(e % a.in[k]);
+        const int w_off = static_cast<int>(a.w_off[k]), b_off = static_cast<int>(a.b_off[k]);
+        const int wsz = a.rows[k] * a.in[k];
+        if (pidx >= w_off && pidx < w_off + wsz) {
+            const unsigned e = static_cast<unsigned>(pidx - w_off);
+            const int r = static_cast<int>(e / static_cast<unsigned>(a.in[k]));
+            const int c = static_cast<int>(e - static_cast<unsigned>(r) * static_cast<unsigned>(a.in[k]));
             for (int s = 0; s < a.nseg[k]; ++s) {
                 const RedSeg& sg = a.seg[k][s];
                 if (c >= sg.col0 && c < sg.col0 + sg.width) {
@@ -1964,17 +1966,24 @@ __global__ void mlp_dw_reduce_kernel(ReduceArgs a) {
                 }
             }
             if (job < 0) return;
-        } else if (pidx >= a.b_off[k] && pidx < a.b_off[k] + a.rows[k]) {
+        } else if (pidx >= b_off && pidx < b_off + a.rows[k]) {
             job = a.bjob[k];
-            row = a.brow0[k] + (pidx - a.b_off[k]);
-            col = static_cast<int64_t>(a.job_KB[job]) * 32;
+            row = a.brow0[k] + (pidx - b_off);
+            col = a.job_KB[job] * 32;
         }
     }
     if (job < 0) return;
-    const int64_t ld = static_cast<int64_t>(a.job_KB[job]) * 32 + 1;
-    const float* s = a.slabs + a.job_slab[job] + row * ld + col;
+    const int ld = a.job_KB[job] * 32 + 1;
+    const float* s = a.slabs + a.job_slab[job] + static_cast<int64_t>(row) * ld + col;
+    const int64_t st = a.slab_floats_per_chunk;
+    // chunk order fixed (deterministic); loads issued four at a time
     float acc = 0.f;
-    for (int c = 0; c < a.chunks; ++c) acc += s[static_cast<int64_t>(c) * a.slab_floats_per_chunk];
+    int c = 0;
+    for (; c + 4 <= a.chunks; c += 4) {
+        const float v0 = s[c * st], v1 = s[(c + 1) * st], v2 = s[(c + 2) * st], v3 = s[(c + 3) * st];
+        acc = (((acc + v0) + v1) + v2) + v3;
+    }
+    for (; c < a.chunks; ++c) acc += s[c * st];
     a.g[pidx] = acc * a.inv_gscale;
 }
 
