@@ -48,11 +48,13 @@ PEAK_HBM_GBS = 8000.0  # HBM3E spec peak; MI355X_MICROARCH.md (~6300 achievable)
 #   dW: it must read every saved layer input and every dz once (HBM-bound; unpadded widths).
 MACS_DX = 128 * (256 + 27) + 256 * 256 + 7 * 256 * 256
 DW_FEATURES = (63 + 8 * 256 + 256 + 27 + 128) + (8 * 256 + 256 + 128 + 1 + 3)
-KERNEL_OF = {"nr_mlp_forward": "mlp_fwd_kernel", "nr_mlp_backward_dx": "mlp_bwd_kernel",
-             "nr_mlp_backward_dw": "mlp_dw_kernel", "nr_mlp_backward_reduce": "mlp_dw_reduce_kernel"}
+# kernels behind each entry point (16-bit forward / dX: the row-block-major kernels)
+KERNEL_OF = {"nr_mlp_forward": ("mlp_fwd_rbm_kernel", "mlp_fwd_kernel"),
+             "nr_mlp_backward_dx": ("mlp_bwd_rbm_kernel", "mlp_bwd_kernel"),
+             "nr_mlp_backward_dw": ("mlp_dw_kernel",), "nr_mlp_backward_reduce": ("mlp_dw_reduce_kernel",)}
 
 
-def traffic_of(kernel: str, M: int, prec: str):
+def traffic_of(kernels, M: int, prec: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC pass
     (profiles/traffic.json, written by tools/traffic.py: 2 x FETCH_SIZE + WRITE_SIZE,
     the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md), or None."""
@@ -60,7 +62,7 @@ def traffic_of(kernel: str, M: int, prec: str):
     if not f.exists():
         return None
     for rec in json.loads(f.read_text()).get("kernels", []):
-        if rec["kernel"] == kernel and rec["M"] == M and rec["precision"] == prec:
+        if rec["kernel"] in kernels and rec["M"] == M and rec["precision"] == prec:
             return rec["bytes_per_launch"]
     return None
 
@@ -362,12 +364,12 @@ def main():
         },
         "roofline": {
             "bound": bound,
-            "kernel": f"{KERNEL_OF.get(entry, entry)} via {entry} (M={M} samples, fine net)",
+            "kernel": f"{KERNEL_OF.get(entry, (entry,))[0]} via {entry} (M={M} samples, fine net)",
             "achieved": round(achieved, 2),
             "peak": peak,
             "unit": unit,
             "frac": round(achieved / peak, 4),
-            "traffic": traffic_of(KERNEL_OF.get(entry, entry), M, args.precision),
+            "traffic": traffic_of(KERNEL_OF.get(entry, (entry,)), M, args.precision),
             "work_per_launch": work,
             "launch_ms": round(ms, 4),
             "launches": n_launch,

@@ -39,7 +39,7 @@ def short(name: str) -> str:
 
 def precision_of(name: str) -> str:
     m = re.search(r"nr::mlp_\w+_kernel<(\d)", name)
-    return {"1": "bf16", "0": "fp32"}.get(m.group(1), "") if m else ""
+    return {"1": "bf16", "0": "fp32", "2": "fp16"}.get(m.group(1), "") if m else ""
 
 
 def sample_count(name: str, grid: int, last_M: int) -> int:
