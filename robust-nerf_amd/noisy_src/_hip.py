@@ -140,9 +140,13 @@ class CallTimer:
     """Brackets selected entry points with HIP events on the launching stream (the
     current torch stream the kernels run on), for per-launch durations in bench.py."""
 
-    def __init__(self, names):
+    def __init__(self, names, keys=None):
         self.names = set(names)
+        self.keys = None if keys is None else set(keys)  # optional: only these name+tag keys
         self.events = {}
+
+    def wants(self, key) -> bool:
+        return self.keys is None or key in self.keys
 
     def record(self, key, fn):
         s = torch.cuda.Event(enable_timing=True)
@@ -169,7 +173,7 @@ def set_timer(timer: Optional[CallTimer]) -> None:
 def call(name: str, *args, tag: str = "") -> int:
     """Invoke an ``nr_*`` entry point and raise RuntimeError on a non-zero code."""
     fn = getattr(load(), name)
-    if _timer is not None and name in _timer.names:
+    if _timer is not None and name in _timer.names and _timer.wants(f"{name}{tag}"):
         rc = _timer.record(f"{name}{tag}", lambda: fn(*args))
     else:
         rc = fn(*args)
