@@ -131,7 +131,7 @@ class Trainer:
             loss_f = ops.mse_loss(out["rgb_fine"], target_rgb)
             loss = loss_c + loss_f
             metrics["loss_fine"] = loss_f
-        loss.backward()
+        loss.backward(ops.unit_grad(loss.device))
         if self.reducer is not None:
             flats = [flat for _, flat in self.reducer.pending]
             self.reducer.finish()
@@ -213,7 +213,7 @@ class PoseTrainer:
                 loss = loss + self.rot_w * torch.mean(cam.rotation_deltas ** 2)
             if self.trans_w > 0 and cam.learn_translation:
                 loss = loss + self.trans_w * torch.mean(cam.translation_deltas ** 2)
-        loss.backward()
+        loss.backward(ops.unit_grad(loss.device))
         if self.reducer is not None:
             flats = [flat for _, flat in self.reducer.pending]
             pg = [p.grad for p in self.poses if p.grad is not None] if optimize_poses else []
