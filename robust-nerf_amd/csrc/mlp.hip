@@ -389,7 +389,9 @@ __device__ __forceinline__ void store_img(char* __restrict__ region, int64_t til
     // wave-uniform base (tile is per wave) + the lane's 16 B: saddr + voffset stores
     char* base = region + ((tile * nblk + blk) * kFPB<PREC>) * static_cast<int64_t>(kFragBytes) + lane16();
     if constexpr (k16<PREC>) {
-#if NR_NT_STORE
+#if defined(NR_NOSTORE_IMG)  // A/B only: keep the values, drop the stores (wrong results)
+        asm volatile("" ::"v"(v.s[0]), "v"(v.s[1]), "v"(base));
+#elif NR_NT_STORE
         // streaming (non-temporal) stores: the 4 GB of images must not evict the
         // L2-resident weight stream every workgroup re-reads
         __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v.s[0]), reinterpret_cast<u32x4*>(base));
