@@ -67,21 +67,97 @@ def traffic_of(kernels, M: int, prec: str):
     return None
 
 
-def roofline_of(entry: str, M: int, ms: float, prec: str, n_params: int):
-    """(bound, achieved, peak, unit, work-per-launch description) of one fused-MLP launch."""
-    esize = 4 if prec == "fp32" else 2
+def rocprof_summary(prec: str):
+    """The committed rocprofv3 kernel-trace summary of the benchmarked tree (the newest
+    profiles/r*_kernel_summary.csv, written by tools/prof_summary.py from the same
+    bench.py command), as {(kernel, M): row}, plus its file name."""
+    import csv
+    files = sorted((ROOT / "profiles").glob("r*_kernel_summary.csv"), key=lambda f: f.stat().st_mtime)
+    files = sorted(files, key=lambda f: f.name.split("_kernel_summary")[0])
+    if not files:
+        return {}, None
+    rows = {}
+    with open(files[-1]) as fh:
+        for r in csv.DictReader(fh):
+            if r.get("M_samples") and r.get("precision", prec) == prec:
+                rows[(r["kernel"], int(r["M_samples"]))] = r
+    return rows, f"profiles/{files[-1].name}"
+
+
+def _flops_of(entry: str, M: int) -> float:
     if entry == "nr_mlp_forward":
-        return "mfma", 2.0 * MACS_PER_EVAL * M / (ms * 1e-3) / 1e12, PEAK_TFLOPS[prec], "TFLOP/s", \
-            f"2 x {MACS_PER_EVAL} MAC x {M} samples"
+        return 2.0 * MACS_PER_EVAL * M
     if entry == "nr_mlp_backward_dx":
-        return "mfma", 2.0 * MACS_DX * M / (ms * 1e-3) / 1e12, PEAK_TFLOPS[prec], "TFLOP/s", \
-            f"2 x {MACS_DX} MAC x {M} samples"
+        return 2.0 * MACS_DX * M
+    return 0.0
+
+
+def _alg_bytes_of(entry: str, M: int, prec: str, n_params: int) -> float:
+    esize = 4 if prec == "fp32" else 2
+    if entry == "nr_mlp_backward_dw":
+        return DW_FEATURES * esize * M + 4 * n_params
+    if entry == "nr_mlp_backward_reduce":
+        return 4 * n_params * 2
+    return 0.0
+
+
+def bound_of(entry: str, M: int, prec: str, counted_bytes):
+    """The roofline that bounds one launch: the larger of its MFMA floor (algorithmic
+    FLOPs / dense peak) and its HBM floor (counted PMC bytes -- or the algorithmic
+    bytes where there are none -- / 8 TB/s).  The training forward and dX are MFMA work
+    whose saved-image / dz stores make the HBM floor the higher one."""
+    t_mfma = _flops_of(entry, M) / (PEAK_TFLOPS[prec] * 1e12)
+    nbytes = counted_bytes if counted_bytes else _alg_bytes_of(entry, M, prec, 0)
+    t_hbm = (nbytes or 0.0) / (PEAK_HBM_GBS * 1e9)
+    return ("hbm" if t_hbm >= t_mfma else "mfma"), t_mfma * 1e3, t_hbm * 1e3
+
+
+def roofline_of(entry: str, M: int, ms: float, prec: str, n_params: int, counted_bytes=None):
+    """(bound, achieved, peak, unit, work-per-launch description) of one fused-MLP launch.
+    ``achieved`` is ALGORITHMIC work (FLOPs, or the bytes the kernel must move) per
+    launch over the launch time, against the peak of the bound that ``bound_of`` picks."""
+    esize = 4 if prec == "fp32" else 2
+    bound, _, _ = bound_of(entry, M, prec, counted_bytes)
+    if entry in ("nr_mlp_forward", "nr_mlp_backward_dx") and bound == "mfma":
+        macs = MACS_PER_EVAL if entry == "nr_mlp_forward" else MACS_DX
+        return "mfma", 2.0 * macs * M / (ms * 1e-3) / 1e12, PEAK_TFLOPS[prec], "TFLOP/s", \
+            f"2 x {macs} MAC x {M} samples"
+    if entry in ("nr_mlp_forward", "nr_mlp_backward_dx"):
+        # byte-bound MFMA kernel: the bytes it must move are its stores (saved images / dz)
+        return "hbm", counted_bytes / (ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s", \
+            f"{counted_bytes:.0f} counted HBM bytes (PMC, profiles/traffic.json)"
     if entry == "nr_mlp_backward_dw":
         nbytes = DW_FEATURES * esize * M + 4 * n_params
         return "hbm", nbytes / (ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s", \
             f"{DW_FEATURES} features x {esize} B x {M} samples + {n_params} fp32 grads"
     nbytes = 4 * n_params * 2
     return "hbm", nbytes / (ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s", f"{n_params} fp32 grads"
+
+
+def kernel_table(wcalls, prec: str, n_params: int, steps_per_key=1):
+    """Per fused-MLP launch key: live ms, counted HBM bytes (PMC), the counted-byte rate,
+    MFMA / HBM floors and the bound; plus the step's counted MLP bytes."""
+    out, step_bytes = {}, 0.0
+    for key, (n, ms) in sorted(wcalls.items()):
+        entry, M = key.split("[M=")[0], int(key.split("[M=")[1].rstrip("]"))
+        kern = KERNEL_OF.get(entry, (entry,))
+        tb = traffic_of(kern, M, prec if entry != "nr_mlp_backward_reduce" else "")
+        bound, f_mfma, f_hbm = bound_of(entry, M, prec, tb)
+        rec = {"ms": round(ms, 4), "bound": bound, "mfma_floor_ms": round(f_mfma, 4), "hbm_floor_ms": round(f_hbm, 4)}
+        fl = _flops_of(entry, M)
+        if fl:
+            rec["mfma_tflops"] = round(fl / (ms * 1e-3) / 1e12, 1)
+            rec["mfma_frac"] = round(fl / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[prec], 4)
+        if tb:
+            rec["counted_bytes"] = tb
+            rec["counted_GBps"] = round(tb / (ms * 1e-3) / 1e9, 1)
+            rec["counted_hbm_frac"] = round(tb / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+            step_bytes += tb
+        alg = _alg_bytes_of(entry, M, prec, n_params)
+        if alg and tb:
+            rec["counted_over_algorithmic"] = round(tb / alg, 4)
+        out[key] = rec
+    return out, step_bytes
 
 
 def lego_rays(n_rays: int, seed: int, device, size: int = 800):
@@ -228,11 +304,96 @@ def batch_assembly_ms(device, B: int, steps: int = 50):
     return out
 
 
+EVAL_METRIC = "eval render rays/sec (render_image of a full test view, chunk 4096), lego 800² 64c+128f"
+
+
+def eval_bench(args, dev, world: int, rank: int, pg):
+    """the eval path of the metric's test PSNR -- ``train.render_image``
+    (reference train.py:122-160 / inference.py:75-105) of a whole 800x800 view of the
+    lego cameras through ``NeRFRenderer`` at the reference's eval chunk of 4096 rays,
+    deterministic (det=True, no perturbation), forward-only fused MLP.  One step = one
+    640,000-ray image; with N ranks each renders its own views (inference.py's test
+    split sharded round-robin)."""
+    from noisy_src import _hip
+    from noisy_src.config import ModelConfig, RenderConfig
+    from noisy_src.model import create_nerf
+    from noisy_src.rendering import NeRFRenderer
+    from noisy_src.train import render_image
+    torch.manual_seed(42)
+    mc, mf = create_nerf(ModelConfig(precision=args.precision))
+    mc, mf = mc.to(dev), mf.to(dev)
+    rcfg = RenderConfig(num_samples=args.num_samples, num_samples_fine=args.num_samples_fine)
+    renderer = NeRFRenderer(mc, mf, rcfg)
+    fix = sorted((ROOT / "tests" / "golden").glob("final_poses_*.npz"))[0]
+    poses = torch.from_numpy(np.load(fix)["ground_truth_poses"]).to(dev)
+    H = W = 800
+    focal = 0.5 * W / math.tan(0.5 * 0.6911112070083618)
+    chunk = args.eval_chunk
+    views = [poses[(rank + world * k) % poses.shape[0]] for k in range(args.warmup + args.steps)]
+    fwd_key = f"nr_mlp_forward[M={chunk * (rcfg.num_samples + rcfg.num_samples_fine)}]"
+    for k in range(args.warmup):
+        render_image(renderer, views[k], H, W, focal, chunk_size=chunk)
+    timer = _hip.CallTimer(["nr_mlp_forward"], keys=[fwd_key])
+    _hip.set_timer(timer)
+    if pg is not None:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        out = render_image(renderer, views[args.warmup + k], H, W, focal, chunk_size=chunk)
+    torch.cuda.synchronize()
+    if pg is not None:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    _hip.set_timer(None)
+    if pg is not None:
+        tt = torch.tensor([dt], device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        dt = float(tt)
+    assert torch.isfinite(out["rgb"]).all()
+    rays = H * W
+    value = world * rays * args.steps / dt
+    evals = rcfg.num_samples + (rcfg.num_samples + rcfg.num_samples_fine)
+    flop_ray = 2.0 * MACS_PER_EVAL * evals  # forward only: 303.8 MFLOP per ray at 64c+128f
+    calls = timer.summary()
+    n_launch, ms = calls.get(fwd_key, (0, float("nan")))
+    Mf = int(fwd_key.split("[M=")[1].rstrip("]"))
+    fine_tf = 2.0 * MACS_PER_EVAL * Mf / (ms * 1e-3) / 1e12
+    return {
+        "metric": EVAL_METRIC,
+        "value": round(value, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * dt / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (random-init networks; lego 800x800 training cameras of the reference's GT poses)",
+        "config": {"workload": f"render_image of one 800x800 view per step per GPU, chunk {chunk}, "
+                               f"{rcfg.num_samples}c+{rcfg.num_samples_fine}f, det=True",
+                   "rays_per_step": rays, "chunk": chunk, "parallelism": f"views sharded over {world} GPU(s)"},
+        "roofline": {"bound": "mfma", "kernel": f"mlp_fwd_rbm_kernel via nr_mlp_forward (M={Mf}, fine net, inference)",
+                     "achieved": round(fine_tf, 1), "peak": PEAK_TFLOPS[args.precision], "unit": "TFLOP/s",
+                     "frac": round(fine_tf / PEAK_TFLOPS[args.precision], 4), "traffic": None,
+                     "work_per_launch": f"2 x {MACS_PER_EVAL} MAC x {Mf} samples", "launch_ms": round(ms, 4),
+                     "launches": n_launch},
+        # whole-render forward MFMA fraction: rays/s x forward FLOP per ray / (GPUs x peak)
+        "flop_per_ray": flop_ray,
+        "step_mfma_frac": round(value * flop_ray / (world * PEAK_TFLOPS[args.precision] * 1e12), 4),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 200; --eval: 10 images)")
+    ap.add_argument("--warmup", type=int, default=None, help="warm-up steps (default 20; --eval: 2 images)")
+    ap.add_argument("--eval", action="store_true",
+                    help="time the eval path instead (render_image of full 800x800 views, chunk 4096)")
+    ap.add_argument("--eval-chunk", type=int, default=4096)
     ap.add_argument("--batch", type=int, default=4096, help="rays per GPU per step")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--num-samples", type=int, default=64)
@@ -245,6 +406,10 @@ def main():
     ap.add_argument("--pose-opt", action="store_true",
                     help="BASELINE cfg #3: joint pose optimisation step (train_pose_opt, poses optimising)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 10 if args.eval else 200
+    if args.warmup is None:
+        args.warmup = 2 if args.eval else 20
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -264,6 +429,14 @@ def main():
         else:
             dist.init_process_group(backend)
         pg = dist.group.WORLD
+
+    if args.eval:
+        out = eval_bench(args, dev, world, rank, pg)
+        if rank == 0:
+            print(json.dumps(out))
+        if pg is not None:
+            torch.distributed.destroy_process_group()
+        return
 
     from noisy_src import _hip
     from noisy_src.config import ModelConfig, RenderConfig
@@ -356,7 +529,16 @@ def main():
         dom_key = max(calls, key=lambda k: calls[k][0] * calls[k][1])
     n_launch, ms = calls[dom_key]  # live, over the timed region
     entry, M = dom_key.split("[M=")[0], int(dom_key.split("[M=")[1].rstrip("]"))
-    bound, achieved, peak, unit, work = roofline_of(entry, M, ms, args.precision, mf.flat_params().numel())
+    kern = KERNEL_OF.get(entry, (entry,))
+    dom_traffic = traffic_of(kern, M, args.precision)
+    n_params = mf.flat_params().numel()
+    bound, achieved, peak, unit, work = roofline_of(entry, M, ms, args.precision, n_params, dom_traffic)
+    # the committed rocprofv3 kernel trace of this tree (same bench command): its average
+    # for the dominant kernel, and the fraction it gives (the live one is `frac`)
+    rp_rows, rp_src = rocprof_summary(args.precision)
+    rp = next((rp_rows[(k, M)] for k in kern if (k, M) in rp_rows), None)
+    rp_ms = float(rp.get("timed_avg_ms") or rp["avg_ms"]) if rp else None
+    ktab, step_bytes = kernel_table(wcalls, args.precision, n_params)
     value = world * B * args.steps / dt
     out = {
         "metric": METRIC,
@@ -384,16 +566,26 @@ def main():
         },
         "roofline": {
             "bound": bound,
-            "kernel": f"{KERNEL_OF.get(entry, (entry,))[0]} via {entry} (M={M} samples, fine net)",
+            "kernel": f"{kern[0]} via {entry} (M={M} samples, fine net)",
             "achieved": round(achieved, 2),
             "peak": peak,
             "unit": unit,
             "frac": round(achieved / peak, 4),
-            "traffic": traffic_of(KERNEL_OF.get(entry, (entry,)), M, args.precision),
+            "traffic": dom_traffic,
             "work_per_launch": work,
             "launch_ms": round(ms, 4),
             "launches": n_launch,
+            "frac_basis": "launch_ms: live HIP events on the launching stream over the timed region",
+            "rocprof_ms": round(rp_ms, 4) if rp_ms else None,
+            "rocprof_source": rp_src if rp_ms else None,
+            "frac_rocprof": round(achieved * ms / rp_ms / peak, 4) if rp_ms else None,
         },
+        # per fused-MLP launch: live ms (last warm-up steps), counted PMC bytes and their
+        # rate, MFMA / HBM floors and the bound they give (profiles/traffic.json)
+        "kernels": ktab,
+        # the step's counted MLP bytes over the step time, against 8 TB/s
+        "step_hbm_bytes": step_bytes or None,
+        "step_hbm_frac": round(step_bytes / (dt / args.steps) / (PEAK_HBM_GBS * 1e9), 4) if step_bytes else None,
         # whole-step MFMA fraction: rays/s x training FLOP/ray / (GPUs x peak)
         "step_mfma_frac": round(value * 6 * MACS_PER_EVAL * (2 * rcfg.num_samples + rcfg.num_samples_fine)
                                 / (world * PEAK_TFLOPS[args.precision] * 1e12), 4),

@@ -68,11 +68,16 @@ int nr_get_rays_bwd(const float* dirs, const float* c2w, int64_t N,
 /* ---- A3: PixelDataset.get_rays_from_pixels  (noisy_src/data_pose_opt.py:83-148,
  *          PixelSampler.get_rays_for_batch :200-223) ---------------------
  * One pass over the batch, no per-image host loop.  img_idx (B,) int64,
- * pix (B,2) fp32 (u,v) pixel coords, poses (n_img,4,4) indexed by img_idx.  */
+ * pix (B,2) fp32 (u,v) pixel coords, poses (n_img,4,4) indexed by img_idx.
+ * Validating mode: bad_index (nullable, one device int the caller zeroes) is
+ * set to 1 when any img_idx lies outside [0, n_img) -- the reference's
+ * poses[idx] raises IndexError there (data_pose_opt.py:105-148); the entry
+ * point stays asynchronous (graph-capturable), so the host wrapper reads the
+ * flag and raises.  Such rays come out NaN either way.                      */
 int nr_rays_from_pixels_fwd(const int64_t* img_idx, const float* pix,
                             const float* poses, int n_img, int H, int W,
                             float focal, int B, float* rays_o, float* rays_d,
-                            nr_stream_t stream);
+                            int* bad_index, nr_stream_t stream);
 /* Backward: g_poses (n_img,4,4) must be zeroed by the caller; it receives
  * dL/dposes summed over the pixels of each image (g_rays_d nullable).  One
  * workgroup per image sums its rays in a fixed order: no atomics, the result is
@@ -110,10 +115,14 @@ int nr_se3_poses_bwd(const float* init_poses, const float* rot_deltas,
 
 /* ---- batch assembly: RaySampler  (noisy_src/data.py:264-321) -----------
  * out_*[b] = table_*[idx[b]] for the (n_rays,3) ray table (rays_o, rays_d,
- * colors) in one launch; idx outside [0, n_rays) gives NaN rows.            */
+ * colors) in one launch; idx outside [0, n_rays) gives NaN rows and, in the
+ * validating mode (bad_index non-NULL, caller-zeroed device int), sets
+ * *bad_index = 1 for the host wrapper to raise IndexError (torch indexing in
+ * the reference's data.py:305-309 raises).                                   */
 int nr_gather_rays(const int64_t* idx, int64_t n_rays, int B,
                    const float* rays_o, const float* rays_d, const float* colors,
-                   float* out_o, float* out_d, float* out_rgb, nr_stream_t stream);
+                   float* out_o, float* out_d, float* out_rgb, int* bad_index,
+                   nr_stream_t stream);
 
 /* ---- A5: sample_along_rays  (noisy_src/rays.py:145-210) ------------------
  * z (B,N); pts (B,N,3) nullable.  t_rand (B,N) nullable -> no perturbation. */

@@ -27,6 +27,19 @@
 #include <type_traits>
 #include <utility>
 
+// Timing-only A/B switches that compute WRONG results (dropped stores, a racing LDS
+// ring, skipped DMA/barriers/MFMAs/bias sums) exist for tools/build_variant.sh, which
+// builds them into noisy_src/lib/variants/ with NR_AB_VARIANT defined.  The product
+// library (Makefile) refuses every one of them, so a stray -D cannot ship.
+#if !defined(NR_AB_VARIANT)
+#if defined(NR_NOSTORE_IMG) || defined(NR_RBM_NOWAIT) || (defined(NR_DW_NOCOMPUTE) && NR_DW_NOCOMPUTE) || \
+    (defined(NR_DW_NOBIAS) && NR_DW_NOBIAS) || (defined(NR_AB_NODMA) && NR_AB_NODMA) ||                   \
+    (defined(NR_AB_NOBAR) && NR_AB_NOBAR) || (defined(NR_AB_NOWAIT) && NR_AB_NOWAIT) ||                   \
+    (defined(NR_AB_HALFA) && NR_AB_HALFA) || (defined(NR_FWD_NOSINK) && NR_FWD_NOSINK)
+#error "wrong-result A/B switch in a product build: build it with tools/build_variant.sh (NR_AB_VARIANT)"
+#endif
+#endif
+
 #include "common.hpp"
 #include "mfma.hpp"
 #include "mlp_plan.hpp"

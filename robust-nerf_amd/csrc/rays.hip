@@ -139,12 +139,13 @@ __device__ __forceinline__ void pixel_dir(const float* pix, int b, int W, int H,
 
 __global__ void rays_from_pixels_fwd_kernel(const int64_t* img_idx, const float* pix, const float* poses,
                                             int n_img, int H, int W, float focal, int B, float* ro,
-                                            float* rd) {
+                                            float* rd, int* bad_index) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     const int64_t img = img_idx[b];
     if (img < 0 || img >= n_img) {  // out-of-range image index: poison the ray, never read out of bounds
         for (int c = 0; c < 3; ++c) ro[3 * b + c] = rd[3 * b + c] = __builtin_nanf("");
+        if (bad_index) *bad_index = 1;  // validating mode: the host wrapper raises IndexError
         return;
     }
     const float* P = poses + 16 * img;
@@ -365,11 +366,13 @@ __global__ void se3_poses_bwd_kernel(const float* init, const float* rot, const 
 // RaySampler (data.py:264-321): rows idx[b] of the device ray table (rays_o,
 // rays_d, colors; 36 B per ray) into one batch, one launch for all three.
 __global__ void gather_rays_kernel(const int64_t* idx, int64_t n_rays, int B, const float* ro, const float* rd,
-                                   const float* rgb, float* out_o, float* out_d, float* out_rgb) {
+                                   const float* rgb, float* out_o, float* out_d, float* out_rgb,
+                                   int* bad_index) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     const int64_t i = idx[b];
     const bool ok = i >= 0 && i < n_rays;
+    if (!ok && bad_index) *bad_index = 1;  // validating mode: the host wrapper raises IndexError
     for (int c = 0; c < 3; ++c) {
         out_o[3 * b + c] = ok ? ro[3 * i + c] : __builtin_nanf("");
         out_d[3 * b + c] = ok ? rd[3 * i + c] : __builtin_nanf("");
@@ -547,11 +550,13 @@ int nr_get_rays_bwd(const float* dirs, const float* c2w, int64_t N, const float*
 }
 
 int nr_rays_from_pixels_fwd(const int64_t* img_idx, const float* pix, const float* poses, int n_img, int H,
-                            int W, float focal, int B, float* ro, float* rd, nr_stream_t stream) {
+                            int W, float focal, int B, float* ro, float* rd, int* bad_index,
+                            nr_stream_t stream) {
     NR_REQUIRE(img_idx && pix && poses && ro && rd && B >= 0 && n_img > 0, "nr_rays_from_pixels_fwd: bad arguments");
     if (B == 0) return NR_OK;
     hipLaunchKernelGGL(rays_from_pixels_fwd_kernel, dim3(ceil_div(B, 256)), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), img_idx, pix, poses, n_img, H, W, focal, B, ro, rd);
+                       static_cast<hipStream_t>(stream), img_idx, pix, poses, n_img, H, W, focal, B, ro, rd,
+                       bad_index);
     NR_LAUNCH_CHECK("nr_rays_from_pixels_fwd");
     return NR_OK;
 }
@@ -601,12 +606,13 @@ int nr_se3_poses_bwd(const float* init, const float* rot, const int64_t* indices
 }
 
 int nr_gather_rays(const int64_t* idx, int64_t n_rays, int B, const float* rays_o, const float* rays_d,
-                   const float* colors, float* out_o, float* out_d, float* out_rgb, nr_stream_t stream) {
+                   const float* colors, float* out_o, float* out_d, float* out_rgb, int* bad_index,
+                   nr_stream_t stream) {
     NR_REQUIRE(idx && rays_o && rays_d && colors && out_o && out_d && out_rgb && B >= 0 && n_rays >= 0,
                "nr_gather_rays: bad arguments");
     if (B == 0) return NR_OK;
     hipLaunchKernelGGL(gather_rays_kernel, dim3(ceil_div(B, 256)), dim3(256), 0, static_cast<hipStream_t>(stream), idx,
-                       n_rays, B, rays_o, rays_d, colors, out_o, out_d, out_rgb);
+                       n_rays, B, rays_o, rays_d, colors, out_o, out_d, out_rgb, bad_index);
     NR_LAUNCH_CHECK("nr_gather_rays");
     return NR_OK;
 }

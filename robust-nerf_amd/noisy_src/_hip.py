@@ -58,12 +58,12 @@ _SIGNATURES = {
     "nr_get_rays": (c_i, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "nr_get_rays_bwd_workspace_bytes": (c_i64, []),
     "nr_get_rays_bwd": (c_i, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "nr_rays_from_pixels_fwd": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_i, c_f, c_i, c_vp, c_vp, c_vp]),
+    "nr_rays_from_pixels_fwd": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_i, c_f, c_i, c_vp, c_vp, c_vp, c_vp]),
     "nr_rays_from_pixels_bwd": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_i, c_f, c_i, c_vp, c_vp, c_vp, c_vp]),
     "nr_se3_poses_fwd": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_vp, c_vp]),
     "nr_check_index_range": (c_i, [c_vp, c_i, c_i, c_vp, c_vp]),
     "nr_se3_poses_bwd": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_vp, c_i, c_vp, c_vp, c_vp]),
-    "nr_gather_rays": (c_i, [c_vp, c_i64, c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "nr_gather_rays": (c_i, [c_vp, c_i64, c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "nr_stratified_sample": (c_i, [c_vp, c_vp, c_vp, c_f, c_f, c_i, c_i, c_i, c_vp, c_vp, c_vp]),
     "nr_positional_encoding": (c_i, [c_vp, c_i64, c_i, c_i, c_i, c_i, c_vp, c_vp]),
     "nr_positional_encoding_bwd": (c_i, [c_vp, c_i64, c_i, c_i, c_i, c_i, c_vp, c_vp, c_vp]),

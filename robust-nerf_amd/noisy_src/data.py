@@ -159,10 +159,17 @@ class RaySampler:
         self._reset_indices()
         return self
 
-    def _gather(self, idx: torch.Tensor) -> dict:
+    def _gather(self, idx: torch.Tensor, validate: bool = False) -> dict:
         ds = self.dataset
-        o, d, rgb = ops.gather_rays(idx, ds.rays_o, ds.rays_d, ds.colors)
+        o, d, rgb = ops.gather_rays(idx, ds.rays_o, ds.rays_d, ds.colors, validate=validate)
         return {"rays_o": o, "rays_d": d, "target_rgb": rgb}
+
+    def get_batch(self, indices: torch.Tensor) -> dict:
+        """The batch of caller-chosen ray indices (the reference's ``rays_o[batch_indices]``
+        ..., data.py:305-309): one gather launch in its validating mode, so an index
+        outside the table raises IndexError as torch indexing does.  The sampler's own
+        draws (randperm / randint) are in range by construction and skip the check."""
+        return self._gather(indices.to(self.device), validate=True)
 
     def __next__(self) -> dict:
         if self.current_idx >= self.n_rays:

@@ -60,8 +60,8 @@ class PixelDataset:
         uniq, inv = torch.unique(pixel_batch.image_indices, return_inverse=True)
         if poses.shape[0] != uniq.shape[0]:
             raise ValueError(f"get_rays_from_pixels: {poses.shape[0]} poses for {uniq.shape[0]} unique images")
-        return ops.rays_from_pixels(inv, pixel_batch.pixel_coords, poses, self.H, self.W, self.focal,
-                                    validate=not pixel_batch.in_range)
+        # ``inv`` indexes ``uniq`` by construction: nothing to validate here
+        return ops.rays_from_pixels(inv, pixel_batch.pixel_coords, poses, self.H, self.W, self.focal, validate=False)
 
 
 class PixelSampler:

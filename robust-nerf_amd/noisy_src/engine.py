@@ -55,6 +55,16 @@ def rank_slice(n_global: int, rank: int, world: int) -> slice:
     return slice(rank * per, (rank + 1) * per)
 
 
+def check_run_args(config, world: int, train_data, val_data) -> None:
+    """Fail before any work for arguments the loops cannot honour: a global batch the
+    ranks cannot split evenly (every batch would be skipped), or only one of
+    train_data / val_data (the loops validate on val_data and train on train_data)."""
+    if world > 1 and config.data.batch_size % world:
+        raise ValueError(f"batch_size {config.data.batch_size} is not divisible by the {world} data-parallel ranks")
+    if (train_data is None) != (val_data is None):
+        raise ValueError("train_data and val_data must be given together (or neither: load the scene from disk)")
+
+
 def mean_over_ranks(values, process_group=None):
     """Average a list of device scalars over the group (the logged global-batch losses)."""
     t = torch.stack([v.detach().float().reshape(()) for v in values])
@@ -76,15 +86,24 @@ def lr_lambda_factory(lr_decay: int):
 
 class GradAllReducer:
     """Bucketed data-parallel gradient averaging: one async all-reduce (SUM) per flat
-    gradient buffer, launched when the buffer is ready; ``finish`` waits and divides by
-    the world size.  Backend-agnostic (RCCL on the GPU box, gloo in the CPU tests)."""
+    gradient buffer, launched when the buffer is ready; ``finish`` waits.  With
+    ``average`` it then divides by the world size; the trainers instead pre-scale the
+    backward seed by 1/world (``prescale``), so the SUM already is the mean and no
+    multiply kernel runs per buffer.  Backend-agnostic (RCCL on the GPU box, gloo in
+    the CPU tests)."""
 
-    def __init__(self, process_group=None):
+    def __init__(self, process_group=None, average: bool = True):
         import torch.distributed as dist
         self.dist = dist
         self.group = process_group
         self.world = dist.get_world_size(process_group)
+        self.average = average
         self.pending = []
+
+    @property
+    def prescale(self) -> float:
+        """The factor the backward seed carries when ``average`` is off."""
+        return 1.0 if self.average else 1.0 / self.world
 
     def launch(self, flat: torch.Tensor) -> None:
         work = self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group, async_op=True)
@@ -93,7 +112,7 @@ class GradAllReducer:
     def finish(self) -> None:
         for work, flat in self.pending:
             work.wait()
-            if self.world > 1:
+            if self.average and self.world > 1:
                 flat.mul_(1.0 / self.world)
         self.pending.clear()
 
@@ -114,7 +133,7 @@ class Trainer:
         self.process_group = process_group
         self.reducer = None
         if process_group is not None:
-            self.reducer = GradAllReducer(process_group)
+            self.reducer = GradAllReducer(process_group, average=False)
             for net in (model_coarse, model_fine):
                 if net is not None:
                     net._grad_ready_hook = self.reducer.launch
@@ -124,11 +143,12 @@ class Trainer:
         self.optimizer.zero_grad(set_to_none=True)
         out = render_rays(self.model_coarse, self.model_fine, rays_o, rays_d, self.render_config, is_train=True,
                           t_rand=t_rand, u=u)
-        loss_c = ops.mse_loss(out["rgb_coarse"], target_rgb)
+        gs = self.reducer.prescale if self.reducer is not None else 1.0  # DP: 1/world in the seed
+        loss_c = ops.mse_loss(out["rgb_coarse"], target_rgb, gs)
         loss = loss_c
         metrics = {"loss_coarse": loss_c}
         if "rgb_fine" in out:
-            loss_f = ops.mse_loss(out["rgb_fine"], target_rgb)
+            loss_f = ops.mse_loss(out["rgb_fine"], target_rgb, gs)
             loss = loss_c + loss_f
             metrics["loss_fine"] = loss_f
         loss.backward(ops.unit_grad(loss.device))
@@ -159,7 +179,9 @@ class PoseTrainer:
     (each rank touches its own images) is one more all-reduce of 2 x 3 x n_poses floats.
     Every gradient is AVERAGED over the ranks: each rank's loss is the mean over its
     equal share of the global batch plus the replicated pose regulariser, so the mean
-    of the rank gradients is the single-process gradient.
+    of the rank gradients is the single-process gradient.  The 1/world
+    rides in the backward seed (the MSE kernels' gradient scale and the regulariser's
+    factor), so the all-reduced SUM is that mean without a multiply per buffer.
     Before the pose-optimisation delay (``optimize_poses=False``) the poses enter the
     step detached: the reference lets their gradient accumulate unused until the first
     optimising step's ``zero_grad``, so skipping it changes
@@ -182,7 +204,7 @@ class PoseTrainer:
                                 if self.optimizer_poses is not None else None)
         self.reducer = None
         if process_group is not None:
-            self.reducer = GradAllReducer(process_group)
+            self.reducer = GradAllReducer(process_group, average=False)
             for net in (model_coarse, model_fine):
                 if net is not None:
                     net._grad_ready_hook = self.reducer.launch
@@ -201,19 +223,27 @@ class PoseTrainer:
         target = pixel_batch.target_rgb
         out = render_rays(self.model_coarse, self.model_fine, rays_o, rays_d, self.render_config, is_train=True,
                           t_rand=t_rand, u=u)
-        loss_c = ops.mse_loss(out["rgb_coarse"], target)
+        gs = self.reducer.prescale if self.reducer is not None else 1.0  # DP: 1/world in the seed
+        loss_c = ops.mse_loss(out["rgb_coarse"], target, gs)
         loss = loss_c
         metrics = {"loss_coarse": loss_c}
         if "rgb_fine" in out:
-            loss_f = ops.mse_loss(out["rgb_fine"], target)
+            loss_f = ops.mse_loss(out["rgb_fine"], target, gs)
             loss = loss_c + loss_f
             metrics["loss_fine"] = loss_f
+        bwd = loss
         if optimize_poses:
+            # the regulariser is replicated on every rank: its gradient carries the seed's
+            # 1/world too, so the SUM over the ranks counts it once
+            reg = []
             if self.rot_w > 0 and cam.learn_rotation:
-                loss = loss + self.rot_w * torch.mean(cam.rotation_deltas ** 2)
+                reg.append(self.rot_w * torch.mean(cam.rotation_deltas ** 2))
             if self.trans_w > 0 and cam.learn_translation:
-                loss = loss + self.trans_w * torch.mean(cam.translation_deltas ** 2)
-        loss.backward(ops.unit_grad(loss.device))
+                reg.append(self.trans_w * torch.mean(cam.translation_deltas ** 2))
+            for r in reg:
+                loss = loss + r
+                bwd = bwd + (r * gs if gs != 1.0 else r)
+        bwd.backward(ops.unit_grad(loss.device))
         if self.reducer is not None:
             flats = [flat for _, flat in self.reducer.pending]
             pg = [p.grad for p in self.poses if p.grad is not None] if optimize_poses else []

@@ -81,15 +81,25 @@ def get_rays(directions: torch.Tensor, c2w: torch.Tensor) -> Tuple[torch.Tensor,
     return _GetRays.apply(directions, c2w)
 
 
-def gather_rays(idx, rays_o, rays_d, colors):
+def _raise_if_flagged(flag: Optional[torch.Tensor], limit: int, what: str) -> None:
+    """The validating mode's host side: one read of the device flag the kernel set."""
+    if flag is not None and int(flag.item()):
+        raise IndexError(f"{what} out of range for {limit} entries")
+
+
+def gather_rays(idx, rays_o, rays_d, colors, validate: bool = False):
     """RaySampler batch assembly (data.py:264-321): the rows idx of the device ray table,
-    all three arrays in one kernel."""
+    all three arrays in one kernel.  ``validate`` (indices from a caller) raises
+    IndexError, as the reference's tensor indexing does, for rows outside the table;
+    the check rides in the gather kernel (one launch, one host read)."""
     _check(idx, rays_o, rays_d, colors)
     i = idx.to(torch.int64).contiguous()
     B = i.shape[0]
     out = [torch.empty(B, 3, device=i.device, dtype=_f32) for _ in range(3)]
+    flag = torch.zeros(1, device=i.device, dtype=torch.int32) if validate else None
     call("nr_gather_rays", ptr(i), rays_o.shape[0], B, ptr(_c(rays_o)), ptr(_c(rays_d)), ptr(_c(colors)),
-         ptr(out[0]), ptr(out[1]), ptr(out[2]), _stream())
+         ptr(out[0]), ptr(out[1]), ptr(out[2]), ptr(flag), _stream())
+    _raise_if_flagged(flag, rays_o.shape[0], "ray index")
     return out
 
 
@@ -278,14 +288,16 @@ def composite(rgb, sigma, z_vals, rays_d, noise=None, white_background=True):
 # ---------------------------------------------------------------- A3 / A4 ----
 class _RaysFromPixels(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, img_idx, pix, poses, H, W, focal):
+    def forward(ctx, img_idx, pix, poses, H, W, focal, validate):
         img = img_idx.to(torch.int64).contiguous()
         px, ps = _c(pix), _c(poses)
         B = img.shape[0]
         ro = torch.empty(B, 3, device=px.device, dtype=_f32)
         rd = torch.empty(B, 3, device=px.device, dtype=_f32)
+        flag = torch.zeros(1, device=px.device, dtype=torch.int32) if validate else None
         call("nr_rays_from_pixels_fwd", ptr(img), ptr(px), ptr(ps), ps.shape[0], H, W, float(focal), B, ptr(ro),
-             ptr(rd), _stream())
+             ptr(rd), ptr(flag), _stream())
+        _raise_if_flagged(flag, ps.shape[0], "image index")
         ctx.save_for_backward(img, px, ps)
         ctx.args = (H, W, float(focal))
         return ro, rd
@@ -300,7 +312,7 @@ class _RaysFromPixels(torch.autograd.Function):
         g_poses = torch.zeros_like(ps)
         call("nr_rays_from_pixels_bwd", ptr(img), ptr(px), ptr(ps), ps.shape[0], H, W, focal, B, ptr(_c(g_ro)),
              ptr(_c(g_rd)), ptr(g_poses), _stream())
-        return None, None, g_poses, None, None, None
+        return None, None, g_poses, None, None, None, None
 
 
 def check_index_range(idx: torch.Tensor, limit: int, what: str = "index") -> None:
@@ -316,12 +328,11 @@ def check_index_range(idx: torch.Tensor, limit: int, what: str = "index") -> Non
 
 def rays_from_pixels(img_idx, pix, poses, H, W, focal, validate: bool = False):
     """get_rays_from_pixels (data_pose_opt.py:83-148) in one pass; poses indexed by img_idx.
-    ``validate`` checks img_idx against poses.shape[0] first (IndexError); unchecked
+    ``validate`` raises IndexError for an img_idx outside [0, poses.shape[0]) (the
+    kernel's validating mode: same launch, one host read of its flag); unchecked
     out-of-range rays come out NaN and get no pose gradient."""
     _check(img_idx, pix, poses)
-    if validate:
-        check_index_range(img_idx, poses.shape[0], "image index")
-    return _RaysFromPixels.apply(img_idx, pix, poses, H, W, focal)
+    return _RaysFromPixels.apply(img_idx, pix, poses, H, W, focal, bool(validate))
 
 
 class _Se3Poses(torch.autograd.Function):
@@ -384,11 +395,13 @@ def adam_step(p, g, m, v, lr, beta1, beta2, eps, step, sumsq=None, max_norm=1.0)
 
 
 class _MSE(torch.autograd.Function):
-    """mean((pred - target)^2) (train.py:89); the gradient is produced in the same kernel."""
+    """mean((pred - target)^2) (train.py:89); the gradient is produced in the same kernel,
+    times ``grad_scale`` (data parallelism folds its 1/world into it: the all-reduced
+    SUM of the ranks' gradients is then the global-batch mean with no extra launch)."""
 
     @staticmethod
-    def forward(ctx, pred, target):
-        loss, g = mse_loss_and_grad(pred, target)
+    def forward(ctx, pred, target, grad_scale):
+        loss, g = mse_loss_and_grad(pred, target, grad_scale)
         ctx.save_for_backward(g)
         return loss
 
@@ -397,8 +410,8 @@ class _MSE(torch.autograd.Function):
         (g,) = ctx.saved_tensors
         # seeded by unit_grad(): gl is exactly 1.0, so g * gl == g (no multiply launch)
         if gl.data_ptr() == _unit.get(gl.device, _NO_UNIT).data_ptr():
-            return g, None
-        return g * gl, None
+            return g, None, None
+        return g * gl, None, None
 
 
 _unit = {}
@@ -417,6 +430,7 @@ def unit_grad(device) -> torch.Tensor:
     return u
 
 
-def mse_loss(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+def mse_loss(pred: torch.Tensor, target: torch.Tensor, grad_scale: float = 1.0) -> torch.Tensor:
+    """The loss value is always the plain mean; only its gradient carries ``grad_scale``."""
     _check(pred, target)
-    return _MSE.apply(pred, target)
+    return _MSE.apply(pred, target, float(grad_scale))

@@ -38,7 +38,7 @@ import torch
 from . import ops
 from .config import NeRFConfig
 from .data import BlenderData, RayDataset, RaySampler, create_data_loaders
-from .engine import Trainer, init_distributed, mean_over_ranks, rank_slice
+from .engine import Trainer, check_run_args, init_distributed, mean_over_ranks, rank_slice
 from .logger import ExperimentLogger, TrainingMetrics, ValidationMetrics
 from .metrics import LPIPSMetric, compute_mse, compute_psnr, compute_ssim
 from .model import create_nerf
@@ -196,6 +196,7 @@ def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
     rank, world = 0, 1
     if process_group is not None:
         rank, world = dist.get_rank(process_group), dist.get_world_size(process_group)
+    check_run_args(config, world, train_data, val_data)
     set_seed(config.train.seed)
     device = config.train.device
     if device.startswith("cuda") and not torch.cuda.is_available():
@@ -253,7 +254,9 @@ def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
                 break
             n = batch["rays_o"].shape[0]
             if world > 1 and n % world:
-                continue  # an epoch's ragged tail cannot be split evenly over the ranks: skipped
+                # only an epoch's short final batch (batch_size % world == 0 is checked
+                # up front): it cannot be split evenly over the ranks, so it is skipped
+                continue
             # the global random draws, in the reference's order (jitter, then inverse-CDF
             # uniforms: rendering.py:161 -> rays.py:204, :255), identical on every rank
             t_rand = torch.rand(n, rc.num_samples, device=device) if rc.perturb else None

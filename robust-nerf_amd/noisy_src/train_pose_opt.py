@@ -40,7 +40,7 @@ from .config import RenderConfig
 from .config import NeRFConfig
 from .data import BlenderData, load_blender_data
 from .data_pose_opt import PixelBatch, PixelSampler, create_pixel_dataset
-from .engine import PoseTrainer, init_distributed, mean_over_ranks, rank_slice
+from .engine import PoseTrainer, check_run_args, init_distributed, mean_over_ranks, rank_slice
 from .logger import ExperimentLogger, TrainingMetrics, ValidationMetrics
 from .metrics import LPIPSMetric, compute_mse, compute_psnr, compute_ssim
 from .model import NeRF
@@ -282,6 +282,7 @@ def train_with_pose_optimization(config: NeRFConfig, noise_config: Optional[Nois
     rank, world = 0, 1
     if process_group is not None:
         rank, world = dist.get_rank(process_group), dist.get_world_size(process_group)
+    check_run_args(config, world, train_data, val_data)
     set_seed(config.train.seed)
     device = config.train.device
     if device.startswith("cuda") and not torch.cuda.is_available():

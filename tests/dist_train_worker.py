@@ -57,6 +57,19 @@ def main():
         trainer.optimizer_poses.step = capture
     else:
         trainer = Trainer(mc, mf, rc, process_group=pg)
+    # the (all-reduced) flat network gradients right before the first Adam step: Adam is
+    # invariant to the gradient's scale, so the parameters alone cannot show a wrong
+    # 1/world; the test compares these with one process's gradients
+    net_grads = []
+    nopt = trainer.optimizer_nerf if pose_mode else trainer.optimizer
+    nstep = nopt.step
+
+    def capture_net(*a, **k):
+        if not net_grads:
+            net_grads.append(torch.cat([p.grad.reshape(-1) for n in (mc, mf) for p in n.parameters()]).cpu())
+        return nstep(*a, **k)
+
+    nopt.step = capture_net
     for k in range(steps):
         g = torch.Generator().manual_seed(900 + k)
         tr = torch.rand(B, rc.num_samples, generator=g).to(dev)
@@ -73,6 +86,7 @@ def main():
         flat = torch.cat([flat, torch.cat([p.detach().reshape(-1).cpu() for p in cam.parameters()])])
         torch.save(torch.stack(pose_grads), out / f"pose_grads_rank{rank}_of{world}.pt")
     torch.save(flat, out / f"{'pose_' if pose_mode else ''}rank{rank}_of{world}.pt")
+    torch.save(net_grads[0], out / f"{'pose_' if pose_mode else ''}net_grads_rank{rank}_of{world}.pt")
     if pg is not None:
         dist.destroy_process_group()
 

@@ -39,6 +39,21 @@ def test_two_ranks_match_one_process(tmp_path):
     # ~0 can flip sign under a different summation order (see test_train_steps_match_oracle)
     assert diff.max() < 2 * steps * 5e-4
     assert (diff < 1e-5).float().mean() > 0.98
+    _assert_net_grads_match(tmp_path, "")
+
+
+def _assert_net_grads_match(tmp_path, prefix):
+    """The all-reduced flat network gradient of step 1 equals, on both ranks, the one
+    process's gradient of the whole batch (to fp32 summation order): a mean-vs-sum or
+    per-slice scale error, invisible after Adam, fails here."""
+    g1 = torch.load(tmp_path / f"{prefix}net_grads_rank0_of1.pt", weights_only=True)
+    g2a = torch.load(tmp_path / f"{prefix}net_grads_rank0_of2.pt", weights_only=True)
+    g2b = torch.load(tmp_path / f"{prefix}net_grads_rank1_of2.pt", weights_only=True)
+    assert torch.equal(g2a, g2b)
+    assert g1.norm() > 0
+    rel = ((g2a.double() - g1.double()).norm() / g1.double().norm()).item()
+    print(f"{prefix or 'train'}: all-reduced network gradient vs one process, rel {rel:.3e}")
+    assert rel <= 1e-5, rel
 
 
 def test_two_ranks_match_one_process_pose_opt(tmp_path):
@@ -69,3 +84,4 @@ def test_two_ranks_match_one_process_pose_opt(tmp_path):
     assert g1.abs().max() > 0
     rel = ((g2a - g1).norm() / g1.norm()).item()
     assert rel < 1e-4, rel
+    _assert_net_grads_match(tmp_path, "pose_")

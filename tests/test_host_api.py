@@ -156,3 +156,21 @@ def test_model_config_envelope_is_checked_at_construction():
     for kw in (dict(num_hidden_layers=4, skips=(1, 2)), dict(pos_freqs=6, dir_freqs=2), dict(skips=()),
                dict(use_view_dirs=False)):
         NeRF(ModelConfig(**kw))
+
+
+def test_run_arguments_fail_fast():
+    """a global batch the data-parallel ranks cannot split, or train_data
+    without val_data, raise ValueError up front in both entry points (instead of an
+    endless loop of skipped batches, or a crash at the first validation)."""
+    from noisy_src.config import NeRFConfig
+    from noisy_src.engine import check_run_args
+    from noisy_src.train import train
+    from noisy_src.train_pose_opt import train_with_pose_optimization
+    cfg = NeRFConfig()
+    cfg.data.batch_size = 1024
+    with pytest.raises(ValueError, match="divisible"):
+        check_run_args(cfg, 3, None, None)
+    check_run_args(cfg, 4, None, None)
+    for fn in (train, train_with_pose_optimization):
+        with pytest.raises(ValueError, match="together"):
+            fn(cfg, train_data=object())

@@ -286,3 +286,28 @@ def test_gather_rays_matches_indexing():
     bad[5] = n
     go, _, _ = ops.gather_rays(bad, o, d, c)
     assert torch.isnan(go[5]).all() and torch.equal(go[6:], o[idx[6:]])
+    # validating mode (indices from a caller): IndexError like the reference's indexing
+    go, _, _ = ops.gather_rays(idx, o, d, c, validate=True)
+    assert torch.equal(go, o[idx])
+    for v in (n, -1):
+        bad[5] = v
+        with pytest.raises(IndexError):
+            ops.gather_rays(bad, o, d, c, validate=True)
+
+
+def test_rays_from_pixels_validating_mode():
+    """nr_rays_from_pixels_fwd's validating mode raises IndexError for an image index
+    outside the pose table (the reference's poses[idx] does), in the same launch."""
+    from noisy_src import ops
+    g = torch.Generator().manual_seed(43)
+    poses = torch.eye(4).repeat(5, 1, 1)
+    poses[:, :3, 3] = torch.randn(5, 3, generator=g)
+    img = torch.randint(0, 5, (300,), generator=g)
+    pix = torch.rand(300, 2, generator=g) * 16
+    o, d = ops.rays_from_pixels(img.to(DEV), pix.to(DEV), poses.to(DEV), 16, 16, 20.0, validate=True)
+    assert torch.equal(o.cpu(), poses[img, :3, 3])
+    img[7] = 5
+    with pytest.raises(IndexError):
+        ops.rays_from_pixels(img.to(DEV), pix.to(DEV), poses.to(DEV), 16, 16, 20.0, validate=True)
+    o, _ = ops.rays_from_pixels(img.to(DEV), pix.to(DEV), poses.to(DEV), 16, 16, 20.0)
+    assert torch.isnan(o[7]).all()

@@ -7,7 +7,7 @@ NAME=$1; shift
 R=/root/repo/robust-nerf_amd
 mkdir -p $R/build/var_$NAME $R/noisy_src/lib/variants
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -ffp-contract=off \
-  -Wno-unused-function -I/root/repo/include -I$R/csrc "$@" -c $R/csrc/mlp.hip -o $R/build/var_$NAME/mlp.o
+  -Wno-unused-function -I/root/repo/include -I$R/csrc -DNR_AB_VARIANT "$@" -c $R/csrc/mlp.hip -o $R/build/var_$NAME/mlp.o
 OBJS=$(ls $R/build/*.o | grep -v "/mlp.o")
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $OBJS $R/build/var_$NAME/mlp.o -o $R/noisy_src/lib/variants/$NAME
 echo built $R/noisy_src/lib/variants/$NAME

@@ -53,7 +53,9 @@ def sample_count(name: str, grid: int, last_M: int) -> int:
     return 0
 
 
-def main(out_dir: str, tag: str) -> None:
+def main(out_dir: str, tag: str, timed_steps: int = 0) -> None:
+    """``timed_steps`` K: also average each fused-MLP key over its last K launches, the
+    launches of bench.py's timed region (each key launches once per step)."""
     base = Path(out_dir)
     rows = defaultdict(list)
     with open(base / "prof" / "run_kernel_trace.csv") as f:
@@ -67,10 +69,13 @@ def main(out_dir: str, tag: str) -> None:
     summ = ROOT / "profiles" / f"{tag}_kernel_summary.csv"
     with open(summ, "w", newline="") as f:
         w = csv.writer(f)
-        w.writerow(["kernel", "grid_threads", "M_samples", "calls", "avg_ms", "median_ms", "total_ms"])
+        w.writerow(["kernel", "precision", "grid_threads", "M_samples", "calls", "avg_ms", "median_ms", "total_ms",
+                    "timed_avg_ms"])
         for (k, g, M), v in sorted(rows.items(), key=lambda kv: -sum(kv[1])):
-            w.writerow([short(k), g, M or "", len(v), f"{statistics.mean(v):.4f}", f"{statistics.median(v):.4f}",
-                        f"{sum(v):.3f}"])
+            timed = v[-timed_steps:] if (timed_steps and M and len(v) >= timed_steps) else []
+            w.writerow([short(k), precision_of(k), g, M or "", len(v), f"{statistics.mean(v):.4f}",
+                        f"{statistics.median(v):.4f}", f"{sum(v):.3f}",
+                        f"{statistics.mean(timed):.4f}" if timed else ""])
     print(f"wrote {summ}")
 
     counters = defaultdict(lambda: defaultdict(list))
@@ -98,7 +103,7 @@ def main(out_dir: str, tag: str) -> None:
                      "fetch_size_bytes": fetch, "write_size_bytes": write,
                      "bytes_per_launch": 2.0 * fetch + write, "launches": len(c["FETCH_SIZE"])})
     out = {"source": f"profiles/{tag}: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                     "python bench.py --steps 2 --warmup 1; traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (median)",
+                     "python bench.py --steps 2 --warmup 1 --no-cpu-baseline; traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (median)",
            "kernels": recs,
            # each (kernel, M) launches once per training step: the step's MLP HBM bytes
            "per_step_mlp_bytes": sum(r["bytes_per_launch"] for r in recs)}
@@ -107,4 +112,4 @@ def main(out_dir: str, tag: str) -> None:
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 0)
