@@ -67,21 +67,37 @@ def traffic_of(kernels, M: int, prec: str):
     return None
 
 
+def source_hash() -> str:
+    """sha1 over the HIP sources and the ABI header (tools/prof_summary.py stamps the same
+    hash into every kernel summary it writes)."""
+    import hashlib
+    h = hashlib.sha1()
+    files = sorted((ROOT / "robust-nerf_amd" / "csrc").glob("*")) + [ROOT / "include" / "nerf_hip.h"]
+    for f in files:
+        if f.suffix in (".hip", ".inc", ".hpp", ".h"):
+            h.update(f.name.encode())
+            h.update(f.read_bytes())
+    return h.hexdigest()[:12]
+
+
 def rocprof_summary(prec: str):
-    """The committed rocprofv3 kernel-trace summary of the benchmarked tree (the newest
-    profiles/r*_kernel_summary.csv, written by tools/prof_summary.py from the same
-    bench.py command), as {(kernel, M): row}, plus its file name."""
+    """The committed rocprofv3 kernel-trace summary of the benchmarked sources: the newest
+    profiles/r*_kernel_summary.csv (tools/prof_summary.py, same bench.py command) whose
+    source_hash equals this tree's, as {(kernel, M): row}, plus its file name."""
     import csv
-    files = sorted((ROOT / "profiles").glob("r*_kernel_summary.csv"), key=lambda f: f.stat().st_mtime)
-    files = sorted(files, key=lambda f: f.name.split("_kernel_summary")[0])
-    if not files:
-        return {}, None
-    rows = {}
-    with open(files[-1]) as fh:
-        for r in csv.DictReader(fh):
-            if r.get("M_samples") and r.get("precision", prec) == prec:
-                rows[(r["kernel"], int(r["M_samples"]))] = r
-    return rows, f"profiles/{files[-1].name}"
+    files = sorted((ROOT / "profiles").glob("r*_kernel_summary.csv"), key=lambda f: f.name.split("_kernel_summary")[0])
+    want = source_hash()
+    for f in reversed(files):
+        rows = {}
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r.get("source_hash") != want:
+                    break
+                if r.get("M_samples") and r.get("precision", prec) == prec:
+                    rows[(r["kernel"], int(r["M_samples"]))] = r
+        if rows:
+            return rows, f"profiles/{f.name}"
+    return {}, None
 
 
 def _flops_of(entry: str, M: int) -> float:
@@ -567,18 +583,22 @@ def main():
         "roofline": {
             "bound": bound,
             "kernel": f"{kern[0]} via {entry} (M={M} samples, fine net)",
-            "achieved": round(achieved, 2),
+            "achieved": round(achieved * ms / rp_ms if rp_ms else achieved, 2),
             "peak": peak,
             "unit": unit,
-            "frac": round(achieved / peak, 4),
+            # frac: from the committed rocprof kernel-trace average of these sources when
+            # one exists (reproducible from profiles/), else from the live launch time
+            "frac": round((achieved * ms / rp_ms if rp_ms else achieved) / peak, 4),
+            "frac_basis": (f"rocprof_ms: timed-region average of {rp_src} (same source_hash)" if rp_ms
+                           else "launch_ms: live HIP events on the launching stream over the timed region"),
             "traffic": dom_traffic,
             "work_per_launch": work,
             "launch_ms": round(ms, 4),
             "launches": n_launch,
-            "frac_basis": "launch_ms: live HIP events on the launching stream over the timed region",
+            "frac_live": round(achieved / peak, 4),
             "rocprof_ms": round(rp_ms, 4) if rp_ms else None,
             "rocprof_source": rp_src if rp_ms else None,
-            "frac_rocprof": round(achieved * ms / rp_ms / peak, 4) if rp_ms else None,
+            "source_hash": source_hash(),
         },
         # per fused-MLP launch: live ms (last warm-up steps), counted PMC bytes and their
         # rate, MFMA / HBM floors and the bound they give (profiles/traffic.json)

@@ -251,6 +251,45 @@ int nr_adam_step(float* params, float* grads, float* exp_avg,
                  double beta2, double eps, int64_t step, const float* sumsq,
                  float max_norm, nr_stream_t stream);
 
+/* The fused optimizer tail of one training step (train.py:112-117: clip_grad_norm_
+ * + optimizer.step(); train_pose_opt.py:398-409 with one clip per network), in two
+ * launches however many flat buffers it covers, and without the re-pack after it:
+ *
+ * nr_sumsq_partials: the nr_sumsq_workspace_bytes() of fixed-order partial sums of
+ * squares over the concatenation of nspan (<= 8) fp32 buffers (one clip group),
+ * written to `partials` (OVERWRITTEN; no caller-zeroed accumulator).          */
+int nr_sumsq_partials(const float* const* xs, const int64_t* ns, int nspan,
+                      float* partials, nr_stream_t stream);
+/* One flat buffer of nr_adam_multi.  sumsq_partials (nullable: no clip) is the
+ * nr_sumsq_partials output of the buffer's clip group, whose grads are scaled by
+ * min(1, max_norm / (sqrt(sum) + 1e-6)) as nr_adam_step does.  pack_table
+ * (nullable) refreshes the MFMA images `packed` of an MLP whose flat parameters
+ * are `params`: every updated parameter is written, converted as nr_mlp_pack
+ * converts it, to each image position the table lists, so `packed` equals
+ * nr_mlp_pack(params) afterwards when it did before (bit-identical).          */
+typedef struct NrAdamSpan {
+    float* params;
+    float* grads;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t n;
+    const float* sumsq_partials;
+    float max_norm;
+    const uint32_t* pack_table;
+    void* packed;
+} NrAdamSpan;
+/* torch.optim.Adam over nspan (<= 8) buffers of one param group (same lr and
+ * 1-based step), one launch.                                                 */
+int nr_adam_multi(const NrAdamSpan* spans, int nspan, double lr, double beta1,
+                  double beta2, double eps, int64_t step, nr_stream_t stream);
+/* The destination table of an MLP's packed images for nr_adam_multi: for each
+ * of the nr_mlp_param_count() flat parameters, 3 slots of (kind << 29 | byte
+ * offset in packed), slot-major (table[s * n + i]); built once per config by
+ * the index maps of nr_mlp_pack itself.                                     */
+int64_t nr_mlp_pack_table_bytes(const NrMlpConfig* cfg);
+int nr_mlp_pack_table(const NrMlpConfig* cfg, uint32_t* table,
+                      nr_stream_t stream);
+
 /* ---- per-ray glue used by render_rays (rendering.py:119-240) ------------ */
 /* viewdirs = d/|d| broadcast to every sample: out (B*S,3). */
 int nr_expand_viewdirs(const float* rays_d, int B, int S, float* out,

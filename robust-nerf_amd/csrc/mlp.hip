@@ -23,6 +23,7 @@
 // over the lanes of those images; it stages whole tiles in LDS (LDS-DMA) and
 // rebuilds sample-major operands with the gfx950 transpose read
 // ds_read_b64_tr_b16 (bf16) or strided ds_read_b32 (fp32).
+#include <cmath>
 #include <cstring>
 #include <type_traits>
 #include <utility>
@@ -43,6 +44,7 @@
 #include "common.hpp"
 #include "mfma.hpp"
 #include "mlp_plan.hpp"
+#include "optim.hpp"
 
 #include "mlp_plan.cpp.inc"
 
@@ -1623,6 +1625,9 @@ __global__ __launch_bounds__(kDinNT) void mlp_dinput_kernel(DinArgs a) {
 #ifndef NR_DW_NSTAGE
 #define NR_DW_NSTAGE 4  // LDS staging ring depth of the dW kernel (tiles)
 #endif
+#ifndef NR_DW_AUX
+#define NR_DW_AUX 0  // cache-policy bits of the dW staging loads (2: nt)
+#endif
 #ifndef NR_DW_ONESHAPE
 #define NR_DW_ONESHAPE 0  // A/B only: every 16-bit wave share runs as 5x2
 #endif
@@ -1748,7 +1753,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     // per piece and tile made this kernel SALU-bound).
     const int total = (NBz + KB) * FPB;
     const int per_wave = (total + kDwWaves - 1) / kDwWaves;
-    constexpr int kMaxPW = k16<PREC> ? 6 : 10;
+    constexpr int kMaxPW = dw_max_pieces(k16<PREC>);  // the plan keeps per_wave <= kMaxPW
     const char* psrc[kMaxPW];
     int64_t pstride[kMaxPW];
     int pdst[kMaxPW];  // LDS offset within a stage, or -1: scratch KB
@@ -1779,7 +1784,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
             if (k < per_wave) {
                 char* d = pdst[k] < 0 ? scratch : dst + pdst[k];
                 __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(psrc[k]),
-                                                 (__attribute__((address_space(3))) void*)(d), 16, 0, 0);
+                                                 (__attribute__((address_space(3))) void*)(d), 16, 0, NR_DW_AUX);
                 psrc[k] += pstride[k];
             }
         }
@@ -2003,6 +2008,25 @@ __global__ void mlp_dw_reduce_kernel(ReduceArgs a) {
 }
 
 // ---------------------------------------------------------------- pack ----
+// Every pack kernel has an index mode (IDX): instead of writing a parameter's value
+// into an image it records where it goes, in the destination table of the fused
+// optimizer step (nr_adam_multi): table[slot * n + i] = kind << 29 | byte offset
+// for flat parameter i.  Slot 0: the forward W image, a bias fragment or a pair
+// image; 1: the W^T image or a vector image; 2: the 16-bit dX-chain image.  The
+// same index maps fill both, so a refresh through the table writes exactly the
+// bytes nr_mlp_pack writes.
+constexpr int kPackSlots = 3;
+enum : uint32_t { kDstNone = 0, kDstF32 = 1, kDstBf16 = 2, kDstF16 = 3, kDstFragBf16 = 4, kDstFragF16 = 5 };
+constexpr int64_t kDstMaxOff = int64_t(1) << 29;
+struct PackIdx {
+    uint32_t* table;
+    int64_t n;  // flat parameters
+};
+__device__ __forceinline__ void put_dst(const PackIdx& t, int slot, int64_t pidx, int64_t off, uint32_t kind) {
+    t.table[slot * t.n + pidx] = (kind << 29) | static_cast<uint32_t>(off);
+}
+__device__ __forceinline__ uint32_t dst16(int prec) { return prec == NR_PREC_FP16 ? kDstF16 : kDstBf16; }
+
 // Image element e of layer l (fwd: W, bwd: W^T), chunk-major:
 //   e = (((kblock * ROWBLOCKS + rowblock) * FPB + frag) * 64 + lane) * EPL + el
 struct PackArgs {
@@ -2031,7 +2055,8 @@ __device__ __forceinline__ int pack_col(const PackArgs& a, int l, int kb, int c)
     return -1;
 }
 
-__global__ void mlp_pack_kernel(PackArgs a) {
+template <bool IDX>
+__global__ void mlp_pack_kernel(PackArgs a, PackIdx t) {
     const int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (g >= a.cum[a.n_lin]) return;
     int l = 0;
@@ -2065,6 +2090,12 @@ __global__ void mlp_pack_kernel(PackArgs a) {
         row = 32 * ob + kk;
         col = pack_col(a, l, ib, i);
     }
+    if constexpr (IDX) {
+        if (col >= 0)
+            put_dst(t, bwd ? 1 : 0, a.w_off[l] + static_cast<int64_t>(row) * a.in[l] + col,
+                    (bwd ? a.pkb[l] : a.pk[l]) + dst_e * (bf ? 2 : 4), bf ? dst16(a.prec) : kDstF32);
+        return;
+    }
     const float v = col >= 0 ? a.params[a.w_off[l] + static_cast<int64_t>(row) * a.in[l] + col] : 0.f;
     char* dst = a.packed + (bwd ? a.pkb[l] : a.pk[l]);
     if (bf)
@@ -2087,7 +2118,8 @@ struct PackBwdrArgs {
     int64_t cum[kMaxMfmaLayers + 1];       // element prefix over layers l0..
 };
 
-__global__ void mlp_pack_bwdr_kernel(PackBwdrArgs a) {
+template <bool IDX>
+__global__ void mlp_pack_bwdr_kernel(PackBwdrArgs a, PackIdx t) {
     const int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (g >= a.cum[a.n_lin]) return;
     int l = a.l0;
@@ -2101,6 +2133,10 @@ __global__ void mlp_pack_bwdr_kernel(PackBwdrArgs a) {
     const int h = lane >> 5, i = lane & 31;
     const int kk = 16 * sub + 8 * (el >> 2) + 4 * h + (el & 3);
     const int row = 32 * ob + kk, col = a.hcol0[l] + 32 * ib + i;
+    if constexpr (IDX) {
+        if (row < a.out[l]) put_dst(t, 2, a.w_off[l] + static_cast<int64_t>(row) * a.in[l] + col, a.pk[l] + 2 * e, dst16(a.prec));
+        return;
+    }
     const float v = row < a.out[l] ? a.params[a.w_off[l] + static_cast<int64_t>(row) * a.in[l] + col] : 0.f;
     unsigned short* dst = reinterpret_cast<unsigned short*>(a.packed + a.pk[l]);
     dst[e] = a.prec == NR_PREC_FP16 ? __builtin_bit_cast(unsigned short, static_cast<_Float16>(v)) : bf16_bits(v);
@@ -2117,22 +2153,30 @@ struct PackBiasArgs {
     int NB[kMaxMfmaLayers], KB[kMaxMfmaLayers], out[kMaxMfmaLayers];
 };
 
-template <int PREC>
-__device__ void pack_bias_one(const PackBiasArgs& a, int l, int nb, int lane) {
+template <int PREC, bool IDX>
+__device__ void pack_bias_one(const PackBiasArgs& a, const PackIdx& t, int l, int nb, int lane) {
     const int row = 32 * nb + lane;
+    if constexpr (IDX) {
+        if (lane < 32 && row < a.out[l])
+            put_dst(t, 0, a.b_off[l] + row,
+                    a.pk[l] + (static_cast<int64_t>(nb) * (2 * a.KB[l] + 1) + 2 * a.KB[l]) * kFragBytes + 16 * lane,
+                    PREC == NR_PREC_FP16 ? kDstFragF16 : kDstFragBf16);
+        return;
+    }
     const float b = (lane < 32 && row < a.out[l]) ? a.params[a.b_off[l] + row] : 0.f;
     const bf16x8 f = bias_frag<PREC>(b);
     char* dst = a.packed + a.pk[l] + (static_cast<int64_t>(nb) * (2 * a.KB[l] + 1) + 2 * a.KB[l]) * kFragBytes;
     reinterpret_cast<bf16x8*>(dst)[lane] = lane < 32 ? f : bf16x8{};
 }
 
-__global__ void mlp_pack_bias_kernel(PackBiasArgs a) {
+template <bool IDX>
+__global__ void mlp_pack_bias_kernel(PackBiasArgs a, PackIdx t) {
     const int l = blockIdx.x / kMaxTrunk, nb = blockIdx.x % kMaxTrunk, lane = threadIdx.x;
     if (l >= a.n_lin || nb >= a.NB[l]) return;
     if (a.prec == NR_PREC_FP16)
-        pack_bias_one<NR_PREC_FP16>(a, l, nb, lane);
+        pack_bias_one<NR_PREC_FP16, IDX>(a, t, l, nb, lane);
     else
-        pack_bias_one<NR_PREC_BF16>(a, l, nb, lane);
+        pack_bias_one<NR_PREC_BF16, IDX>(a, t, l, nb, lane);
 }
 
 // Vector images: element idx of a vector of NB blocks <-> feature 32*(idx>>5) + acc_row(idx&15, (idx>>4)&1).
@@ -2145,9 +2189,11 @@ struct PackVecArgs {
     int64_t dst[kMaxMfmaLayers + 8];          // byte offset in packed
     int cum[kMaxMfmaLayers + 9];              // image elements (NB*32) prefix
     int pair[kMaxMfmaLayers + 8];             // 1: pair image (PImg), 0: vector image (VImg)
+    int slot[kMaxMfmaLayers + 8];             // destination-table slot (IDX mode)
 };
 
-__global__ void mlp_pack_vec_kernel(PackVecArgs a) {
+template <bool IDX>
+__global__ void mlp_pack_vec_kernel(PackVecArgs a, PackIdx t) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= a.cum[a.nv]) return;
     int v = 0;
@@ -2155,7 +2201,84 @@ __global__ void mlp_pack_vec_kernel(PackVecArgs a) {
     const int idx = g - a.cum[v];
     const int f = a.pair[v] ? 32 * (idx >> 5) + acc_row((idx >> 1) & 15, idx & 1)
                             : 32 * (idx >> 5) + acc_row(idx & 15, (idx >> 4) & 1);
+    if constexpr (IDX) {
+        if (f < a.len[v]) put_dst(t, a.slot[v], a.src[v] + f, a.dst[v] + 4 * static_cast<int64_t>(idx), kDstF32);
+        return;
+    }
     reinterpret_cast<float*>(a.packed + a.dst[v])[idx] = f < a.len[v] ? a.params[a.src[v] + f] : 0.f;
+}
+
+// ------------------------------------------------- fused optimizer step ----
+// Adam over up to kMaxAdamSpans flat buffers (blockIdx.y = span), the clip
+// coefficient from the span's clip-group partials (nr_sumsq_partials, summed in the
+// fixed block order by every block), and the packed images refreshed through the
+// span's destination table: nr_mlp_pack's four kernels are not run after the step.
+struct AdamSpanDev {
+    float *p, *g, *m, *v;
+    int64_t n;
+    const float* partials;
+    float max_norm;
+    const uint32_t* table;
+    char* packed;
+};
+struct AdamMultiArgs {
+    AdamSpanDev s[kMaxAdamSpans];
+    float omb1, b2, omb2, eps, step_size, bc2_sqrt;
+};
+
+__device__ __forceinline__ void put_image(char* packed, uint32_t e, float p) {
+    char* q = packed + (e & 0x1fffffffu);
+    switch (e >> 29) {
+        case kDstF32: *reinterpret_cast<float*>(q) = p; break;
+        case kDstBf16: *reinterpret_cast<unsigned short*>(q) = bf16_bits(p); break;
+        case kDstF16: *reinterpret_cast<unsigned short*>(q) = __builtin_bit_cast(unsigned short, static_cast<_Float16>(p)); break;
+        case kDstFragBf16: *reinterpret_cast<bf16x8*>(q) = bias_frag<NR_PREC_BF16>(p); break;
+        case kDstFragF16: *reinterpret_cast<bf16x8*>(q) = bias_frag<NR_PREC_FP16>(p); break;
+        default: break;
+    }
+}
+
+__global__ void __launch_bounds__(kSumsqThreads) adam_multi_kernel(AdamMultiArgs a) {
+    const AdamSpanDev& s = a.s[blockIdx.y];
+    const float coef = s.partials ? clip_coef(block_sum_fixed(s.partials[threadIdx.x]), s.max_norm) : 1.0f;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    const int64_t t0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t n = s.n;
+    // 16-B accesses when every buffer (and the table's slot rows) allows them
+    const int64_t n4 = (n % 4 == 0) ? n / 4 : 0;
+    for (int64_t i = t0; i < n4; i += stride) {
+        float4 P = reinterpret_cast<float4*>(s.p)[i], G = reinterpret_cast<float4*>(s.g)[i];
+        float4 M = reinterpret_cast<float4*>(s.m)[i], V = reinterpret_cast<float4*>(s.v)[i];
+        adam_one(P.x, G.x, M.x, V.x, coef, a.omb1, a.b2, a.omb2, a.step_size, a.bc2_sqrt, a.eps);
+        adam_one(P.y, G.y, M.y, V.y, coef, a.omb1, a.b2, a.omb2, a.step_size, a.bc2_sqrt, a.eps);
+        adam_one(P.z, G.z, M.z, V.z, coef, a.omb1, a.b2, a.omb2, a.step_size, a.bc2_sqrt, a.eps);
+        adam_one(P.w, G.w, M.w, V.w, coef, a.omb1, a.b2, a.omb2, a.step_size, a.bc2_sqrt, a.eps);
+        reinterpret_cast<float4*>(s.p)[i] = P;
+        reinterpret_cast<float4*>(s.g)[i] = G;
+        reinterpret_cast<float4*>(s.m)[i] = M;
+        reinterpret_cast<float4*>(s.v)[i] = V;
+        if (s.table) {
+#pragma unroll
+            for (int sl = 0; sl < kPackSlots; ++sl) {
+                const u32x4 e = reinterpret_cast<const u32x4*>(s.table + sl * n)[i];
+                put_image(s.packed, e.x, P.x);
+                put_image(s.packed, e.y, P.y);
+                put_image(s.packed, e.z, P.z);
+                put_image(s.packed, e.w, P.w);
+            }
+        }
+    }
+    for (int64_t i = 4 * n4 + t0; i < n; i += stride) {
+        float P = s.p[i], G = s.g[i], M = s.m[i], V = s.v[i];
+        adam_one(P, G, M, V, coef, a.omb1, a.b2, a.omb2, a.step_size, a.bc2_sqrt, a.eps);
+        s.p[i] = P;
+        s.g[i] = G;
+        s.m[i] = M;
+        s.v[i] = V;
+        if (s.table)
+#pragma unroll
+            for (int sl = 0; sl < kPackSlots; ++sl) put_image(s.packed, s.table[sl * n + i], P);
+    }
 }
 
 }  // namespace nr
@@ -2331,6 +2454,111 @@ int launch_dinput(const MlpPlan& p, const DinArgs& a, hipStream_t s) {
 
 }  // namespace
 
+namespace {
+
+// nr_mlp_pack's four kernels; IDX: their index mode, filling the destination table
+template <bool IDX>
+int launch_pack(const MlpPlan& p, const float* params, void* packed, PackIdx t, hipStream_t s) {
+    const char* what = IDX ? "nr_mlp_pack_table" : "nr_mlp_pack";
+    PackArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.params = params;
+    a.packed = static_cast<char*>(packed);
+    a.n_lin = p.n_lin;
+    a.prec = p.prec;
+    a.cum[0] = 0;
+    for (int l = 0; l < p.n_lin; ++l) {
+        const LinearDesc& d = p.lin[l];
+        a.w_off[l] = d.w_off;
+        a.in[l] = d.in;
+        a.NB[l] = d.NB;
+        a.KB[l] = d.KB;
+        a.nseg[l] = d.nseg;
+        for (int s = 0; s < d.nseg; ++s) {
+            a.seg_col0[l][s] = d.seg[s].col0;
+            a.seg_w[l][s] = d.seg[s].width;
+            a.seg_blk[l][s] = d.seg[s].blocks;
+        }
+        a.pk[l] = d.pk_fwd;
+        a.pkb[l] = d.pk_bwd;
+        a.bwd_rot[l] = (l > 0 && l < p.n_layers && is_skip(p, l - 1)) ? d.seg[0].blocks : 0;
+        const int64_t elems = static_cast<int64_t>(d.NB) * d.KB * 1024;  // 32x32 elements per block
+        a.cum[l + 1] = a.cum[l] + 2 * elems;
+    }
+    const int64_t total = a.cum[p.n_lin];
+    hipLaunchKernelGGL(mlp_pack_kernel<IDX>, dim3(static_cast<unsigned>(ceil_div_ll(total, 256))), dim3(256), 0, s, a, t);
+    NR_LAUNCH_CHECK(what);
+    if (p.prec != NR_PREC_FP32) {
+        PackBiasArgs pb;
+        std::memset(&pb, 0, sizeof(pb));
+        pb.params = params;
+        pb.packed = static_cast<char*>(packed);
+        pb.prec = p.prec;
+        pb.n_lin = p.n_lin;
+        for (int l = 0; l < p.n_lin; ++l) {
+            pb.pk[l] = p.lin[l].pk_fwd;
+            pb.b_off[l] = p.lin[l].b_off;
+            pb.NB[l] = p.lin[l].NB;
+            pb.KB[l] = p.lin[l].KB;
+            pb.out[l] = p.lin[l].out;
+        }
+        hipLaunchKernelGGL(mlp_pack_bias_kernel<IDX>, dim3(p.n_lin * kMaxTrunk), dim3(64), 0, s, pb, t);
+        NR_LAUNCH_CHECK(what);
+        if (p.n_lin > 1) {
+            PackBwdrArgs pr;
+            std::memset(&pr, 0, sizeof(pr));
+            pr.params = params;
+            pr.packed = static_cast<char*>(packed);
+            pr.prec = p.prec;
+            pr.l0 = 1;
+            pr.n_lin = p.n_lin;
+            pr.cum[1] = 0;
+            for (int l = 1; l < p.n_lin; ++l) {
+                const LinearDesc& d = p.lin[l];
+                pr.w_off[l] = d.w_off;
+                pr.pk[l] = d.pk_bwdr;
+                pr.in[l] = d.in;
+                pr.NB[l] = d.NB;
+                pr.out[l] = d.out;
+                // the hidden input columns: after x_enc in a skip layer (cat([x_enc, h])), first otherwise
+                pr.hcol0[l] = (l < p.n_layers && is_skip(p, l - 1)) ? p.pos_dim : 0;
+                pr.cum[l + 1] = pr.cum[l] + static_cast<int64_t>(kHB) * d.NB * 1024;
+            }
+            const int64_t tot = pr.cum[p.n_lin];
+            hipLaunchKernelGGL(mlp_pack_bwdr_kernel<IDX>, dim3(static_cast<unsigned>(ceil_div_ll(tot, 256))), dim3(256),
+                               0, s, pr, t);
+            NR_LAUNCH_CHECK(what);
+        }
+    }
+    PackVecArgs v;
+    std::memset(&v, 0, sizeof(v));
+    v.params = params;
+    v.packed = static_cast<char*>(packed);
+    auto add_vec = [&](int64_t src, int len, int64_t dst, int nblk, int pair, int slot) {
+        v.pair[v.nv] = pair;
+        v.slot[v.nv] = slot;
+        v.src[v.nv] = src;
+        v.len[v.nv] = len;
+        v.dst[v.nv] = dst;
+        v.cum[v.nv + 1] = v.cum[v.nv] + nblk * 32;
+        v.nv++;
+    };
+    // table slots: biases 1 (slot 0 holds their 16-bit fragment), the head weights'
+    // pair images 0 and their vector images 1
+    for (int l = 0; l < p.n_lin; ++l) add_vec(p.lin[l].b_off, p.lin[l].out, p.lin[l].vb, p.lin[l].NB, 0, 1);
+    add_vec(p.sig_w, kHidden, p.vsig, kHB, 1, 0);
+    for (int c = 0; c < 3; ++c)
+        add_vec(p.rgb_w + c * (kHidden / 2), kHidden / 2, p.vrgb + c * (kHidden / 2) * 4, kHB / 2, 1, 0);
+    add_vec(p.sig_w, kHidden, p.vhead, kHB, 0, 1);
+    for (int c = 0; c < 3; ++c)
+        add_vec(p.rgb_w + c * (kHidden / 2), kHidden / 2, p.vhead + 1024 + c * (kHidden / 2) * 4, kHB / 2, 0, 1);
+    hipLaunchKernelGGL(mlp_pack_vec_kernel<IDX>, dim3(ceil_div(v.cum[v.nv], 256)), dim3(256), 0, s, v, t);
+    NR_LAUNCH_CHECK(what);
+    return NR_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int64_t nr_mlp_param_count(const NrMlpConfig* cfg) {
@@ -2360,98 +2588,61 @@ int nr_mlp_pack(const NrMlpConfig* cfg, const float* params, void* packed, nr_st
     if (!plan_or_error(cfg, &p)) return NR_EARG;
     NR_REQUIRE(params && packed, "nr_mlp_pack: null pointer");
     NR_REQUIRE((reinterpret_cast<uintptr_t>(packed) & 15) == 0, "nr_mlp_pack: packed must be 16-byte aligned");
-    PackArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.params = params;
-    a.packed = static_cast<char*>(packed);
-    a.n_lin = p.n_lin;
-    a.prec = p.prec;
-    a.cum[0] = 0;
-    for (int l = 0; l < p.n_lin; ++l) {
-        const LinearDesc& d = p.lin[l];
-        a.w_off[l] = d.w_off;
-        a.in[l] = d.in;
-        a.NB[l] = d.NB;
-        a.KB[l] = d.KB;
-        a.nseg[l] = d.nseg;
-        for (int s = 0; s < d.nseg; ++s) {
-            a.seg_col0[l][s] = d.seg[s].col0;
-            a.seg_w[l][s] = d.seg[s].width;
-            a.seg_blk[l][s] = d.seg[s].blocks;
-        }
-        a.pk[l] = d.pk_fwd;
-        a.pkb[l] = d.pk_bwd;
-        a.bwd_rot[l] = (l > 0 && l < p.n_layers && is_skip(p, l - 1)) ? d.seg[0].blocks : 0;
-        const int64_t elems = static_cast<int64_t>(d.NB) * d.KB * 1024;  // 32x32 elements per block
-        a.cum[l + 1] = a.cum[l] + 2 * elems;
-    }
-    const int64_t total = a.cum[p.n_lin];
+    return launch_pack<false>(p, params, packed, PackIdx{nullptr, 0}, static_cast<hipStream_t>(stream));
+}
+
+int64_t nr_mlp_pack_table_bytes(const NrMlpConfig* cfg) {
+    MlpPlan p;
+    return plan_or_error(cfg, &p) ? static_cast<int64_t>(kPackSlots) * p.param_count * 4 : -1;
+}
+
+int nr_mlp_pack_table(const NrMlpConfig* cfg, uint32_t* table, nr_stream_t stream) {
+    MlpPlan p;
+    if (!plan_or_error(cfg, &p)) return NR_EARG;
+    NR_REQUIRE(table, "nr_mlp_pack_table: null pointer");
+    NR_REQUIRE((reinterpret_cast<uintptr_t>(table) & 15) == 0, "nr_mlp_pack_table: table must be 16-byte aligned");
+    NR_REQUIRE(p.packed_bytes < kDstMaxOff, "nr_mlp_pack_table: packed images beyond 512 MB");
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(mlp_pack_kernel, dim3(static_cast<unsigned>(ceil_div_ll(total, 256))), dim3(256), 0, s, a);
-    NR_LAUNCH_CHECK("nr_mlp_pack");
-    if (p.prec != NR_PREC_FP32) {
-        PackBiasArgs pb;
-        std::memset(&pb, 0, sizeof(pb));
-        pb.params = params;
-        pb.packed = static_cast<char*>(packed);
-        pb.prec = p.prec;
-        pb.n_lin = p.n_lin;
-        for (int l = 0; l < p.n_lin; ++l) {
-            pb.pk[l] = p.lin[l].pk_fwd;
-            pb.b_off[l] = p.lin[l].b_off;
-            pb.NB[l] = p.lin[l].NB;
-            pb.KB[l] = p.lin[l].KB;
-            pb.out[l] = p.lin[l].out;
-        }
-        hipLaunchKernelGGL(mlp_pack_bias_kernel, dim3(p.n_lin * kMaxTrunk), dim3(64), 0, s, pb);
-        NR_LAUNCH_CHECK("nr_mlp_pack");
-        if (p.n_lin > 1) {
-            PackBwdrArgs pr;
-            std::memset(&pr, 0, sizeof(pr));
-            pr.params = params;
-            pr.packed = static_cast<char*>(packed);
-            pr.prec = p.prec;
-            pr.l0 = 1;
-            pr.n_lin = p.n_lin;
-            pr.cum[1] = 0;
-            for (int l = 1; l < p.n_lin; ++l) {
-                const LinearDesc& d = p.lin[l];
-                pr.w_off[l] = d.w_off;
-                pr.pk[l] = d.pk_bwdr;
-                pr.in[l] = d.in;
-                pr.NB[l] = d.NB;
-                pr.out[l] = d.out;
-                // the hidden input columns: after x_enc in a skip layer (cat([x_enc, h])), first otherwise
-                pr.hcol0[l] = (l < p.n_layers && is_skip(p, l - 1)) ? p.pos_dim : 0;
-                pr.cum[l + 1] = pr.cum[l] + static_cast<int64_t>(kHB) * d.NB * 1024;
-            }
-            const int64_t tot = pr.cum[p.n_lin];
-            hipLaunchKernelGGL(mlp_pack_bwdr_kernel, dim3(static_cast<unsigned>(ceil_div_ll(tot, 256))), dim3(256), 0,
-                               s, pr);
-            NR_LAUNCH_CHECK("nr_mlp_pack");
-        }
+    hipError_t e = hipMemsetAsync(table, 0, static_cast<size_t>(kPackSlots) * p.param_count * 4, s);
+    if (e != hipSuccess) {
+        set_error("nr_mlp_pack_table: %s", hipGetErrorString(e));
+        return static_cast<int>(e);
     }
-    PackVecArgs v;
-    std::memset(&v, 0, sizeof(v));
-    v.params = params;
-    v.packed = static_cast<char*>(packed);
-    auto add_vec = [&](int64_t src, int len, int64_t dst, int nblk, int pair = 0) {
-        v.pair[v.nv] = pair;
-        v.src[v.nv] = src;
-        v.len[v.nv] = len;
-        v.dst[v.nv] = dst;
-        v.cum[v.nv + 1] = v.cum[v.nv] + nblk * 32;
-        v.nv++;
-    };
-    for (int l = 0; l < p.n_lin; ++l) add_vec(p.lin[l].b_off, p.lin[l].out, p.lin[l].vb, p.lin[l].NB);
-    add_vec(p.sig_w, kHidden, p.vsig, kHB, 1);
-    for (int c = 0; c < 3; ++c)
-        add_vec(p.rgb_w + c * (kHidden / 2), kHidden / 2, p.vrgb + c * (kHidden / 2) * 4, kHB / 2, 1);
-    add_vec(p.sig_w, kHidden, p.vhead, kHB);
-    for (int c = 0; c < 3; ++c)
-        add_vec(p.rgb_w + c * (kHidden / 2), kHidden / 2, p.vhead + 1024 + c * (kHidden / 2) * 4, kHB / 2);
-    hipLaunchKernelGGL(mlp_pack_vec_kernel, dim3(ceil_div(v.cum[v.nv], 256)), dim3(256), 0, s, v);
-    NR_LAUNCH_CHECK("nr_mlp_pack");
+    return launch_pack<true>(p, nullptr, nullptr, PackIdx{table, p.param_count}, s);
+}
+
+int nr_adam_multi(const NrAdamSpan* spans, int nspan, double lr, double b1, double b2, double eps, int64_t step,
+                  nr_stream_t stream) {
+    NR_REQUIRE(spans && nspan >= 1 && nspan <= kMaxAdamSpans && step >= 1,
+               "nr_adam_multi: bad arguments (1..%d spans, step >= 1)", kMaxAdamSpans);
+    AdamMultiArgs a;
+    std::memset(&a, 0, sizeof(a));
+    int64_t nmax = 0;
+    for (int k = 0; k < nspan; ++k) {
+        const NrAdamSpan& x = spans[k];
+        NR_REQUIRE(x.params && x.grads && x.exp_avg && x.exp_avg_sq && x.n >= 0, "nr_adam_multi: span %d: null buffer", k);
+        NR_REQUIRE(((reinterpret_cast<uintptr_t>(x.params) | reinterpret_cast<uintptr_t>(x.grads) |
+                     reinterpret_cast<uintptr_t>(x.exp_avg) | reinterpret_cast<uintptr_t>(x.exp_avg_sq) |
+                     reinterpret_cast<uintptr_t>(x.pack_table)) & 15) == 0,
+                   "nr_adam_multi: span %d: buffers must be 16-byte aligned", k);
+        NR_REQUIRE(!x.pack_table || x.packed, "nr_adam_multi: span %d: pack_table without packed", k);
+        a.s[k] = AdamSpanDev{x.params, x.grads, x.exp_avg, x.exp_avg_sq, x.n, x.sumsq_partials, x.max_norm,
+                             x.pack_table, static_cast<char*>(x.packed)};
+        nmax = x.n > nmax ? x.n : nmax;
+    }
+    if (nmax == 0) return NR_OK;
+    // bias corrections in double on the host, as torch's _single/_multi_tensor_adam do
+    const double bc1 = 1.0 - std::pow(b1, static_cast<double>(step));
+    const double bc2 = 1.0 - std::pow(b2, static_cast<double>(step));
+    a.omb1 = static_cast<float>(1.0 - b1);
+    a.b2 = static_cast<float>(b2);
+    a.omb2 = static_cast<float>(1.0 - b2);
+    a.eps = static_cast<float>(eps);
+    a.step_size = static_cast<float>(lr / bc1);
+    a.bc2_sqrt = static_cast<float>(std::sqrt(bc2));
+    const int grid = stream_grid(ceil_div_ll(nmax, 4), kSumsqThreads);
+    hipLaunchKernelGGL(adam_multi_kernel, dim3(grid, nspan), dim3(kSumsqThreads), 0, static_cast<hipStream_t>(stream), a);
+    NR_LAUNCH_CHECK("nr_adam_multi");
     return NR_OK;
 }
 
@@ -2709,6 +2900,8 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
         }
         w.job_nseg[j] = ns;
         w.job_slab[j] = jb.slab_off;
+        NR_REQUIRE((jb.NBz + jb.KB) * p.fpb <= kDwWaves * dw_max_pieces(p.fpb == 2),
+                   "nr_mlp_backward_dw: job %d stages %d blocks, beyond the kernel's per-wave pieces", j, jb.NBz + jb.KB);
         max_blk = jb.NBz + jb.KB > max_blk ? jb.NBz + jb.KB : max_blk;
     }
     w.stage_bytes = max_blk * p.fpb * kFragBytes;

@@ -30,6 +30,9 @@ constexpr int kMaxJobs = kMaxTrunk + 8;  // dW jobs: x-jobs + trunk h-jobs + fea
 constexpr int kMaxSeg = 2;
 constexpr int kMaxJobSeg = 4;            // tensors on either side of a dW job
 constexpr int kMaxRed = kMaxTrunk + 4;    // reduce ranges: trunk, feat, sigma, rgb, dir
+// dW staging: each of the 8 waves issues at most this many 1-KB LDS-DMA pieces
+// per tile, so a job's (NBz + KB) * FPB blocks must not exceed 8x it
+__host__ __device__ constexpr int dw_max_pieces(bool k16) { return k16 ? 6 : 10; }
 
 // One input segment of a linear layer: columns [col0, col0+width) of W,
 // occupying ceil(width/32) consecutive 32-wide input blocks.

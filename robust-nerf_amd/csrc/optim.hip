@@ -14,24 +14,9 @@
 // bit-identical from run to run (the reference is bit-deterministic).
 #include <cmath>
 
-#include "common.hpp"
+#include "optim.hpp"
 
 namespace nr {
-
-constexpr int kSumsqBlocks = 256;
-constexpr int kSumsqThreads = 256;
-static_assert(kSumsqBlocks == kSumsqThreads, "the final pass reads one partial per thread");
-
-// Sum of a block's values in a fixed order: wave butterfly, then waves in index order.
-__device__ __forceinline__ float block_sum_fixed(float s) {
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    __shared__ float part[kSumsqThreads / 64];
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
-    __syncthreads();
-    float t = 0.f;
-    for (int i = 0; i < kSumsqThreads / 64; ++i) t += part[i];
-    return t;
-}
 
 __global__ void __launch_bounds__(kSumsqThreads) sumsq_partial_kernel(const float* x, int64_t n, float* partials) {
     float s = 0.f;
@@ -48,29 +33,41 @@ __global__ void __launch_bounds__(kSumsqThreads) sumsq_partial_kernel(const floa
     if (threadIdx.x == 0) partials[blockIdx.x] = t;
 }
 
+// One clip group's buffers as one sequence: block b sums the elements it strides over
+// in every span, in span order, so the partials are a fixed function of the inputs.
+struct SumsqSpans {
+    const float* x[kMaxAdamSpans];
+    int64_t n[kMaxAdamSpans];
+    int nspan;
+};
+
+__global__ void __launch_bounds__(kSumsqThreads) sumsq_spans_kernel(SumsqSpans sp, float* partials) {
+    float s = 0.f;
+    const int64_t stride = static_cast<int64_t>(kSumsqBlocks) * kSumsqThreads;
+    const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kSumsqThreads + threadIdx.x;
+    for (int k = 0; k < sp.nspan; ++k) {
+        const float* x = sp.x[k];
+        const int64_t n = sp.n[k], n4 = ((reinterpret_cast<uintptr_t>(x) & 15) == 0) ? n / 4 : 0;
+        const float4* x4 = reinterpret_cast<const float4*>(x);
+        for (int64_t i = t0; i < n4; i += stride) {
+            const float4 v = x4[i];
+            s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        }
+        for (int64_t i = 4 * n4 + t0; i < n; i += stride) s += x[i] * x[i];
+    }
+    const float t = block_sum_fixed(s);
+    if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
 __global__ void __launch_bounds__(kSumsqThreads) sumsq_final_kernel(const float* partials, float* acc) {
     const float t = block_sum_fixed(partials[threadIdx.x]);
     if (threadIdx.x == 0) *acc += t;
 }
 
-__device__ __forceinline__ void adam_one(float& p, float& g, float& m, float& v, float coef, float omb1, float b2,
-                                         float omb2, float step_size, float bc2_sqrt, float eps) {
-    g = g * coef;
-    m = m + omb1 * (g - m);  // exp_avg.lerp_(grad, 1 - beta1)
-    v = v * b2 + (omb2 * g) * g;  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
-    const float denom = sqrtf(v) / bc2_sqrt + eps;
-    p = p - step_size * (m / denom);
-}
-
 __global__ void adam_kernel(float* p, float* g, float* m, float* v, int64_t n, float omb1, float b2, float omb2,
                             float eps,
                             float step_size, float bc2_sqrt, const float* sumsq, float max_norm) {
-    float coef = 1.0f;
-    if (sumsq) {
-        const float total = sqrtf(*sumsq);
-        const float c = max_norm / (total + 1e-6f);
-        coef = c < 1.0f ? c : 1.0f;
-    }
+    const float coef = sumsq ? clip_coef(*sumsq, max_norm) : 1.0f;
     const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
     const int64_t n4 = n / 4;
     float4* p4 = reinterpret_cast<float4*>(p);
@@ -111,6 +108,23 @@ int nr_sumsq(const float* x, int64_t n, float* acc, void* workspace, nr_stream_t
     hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(kSumsqThreads), 0, static_cast<hipStream_t>(stream),
                        partials, acc);
     NR_LAUNCH_CHECK("nr_sumsq");
+    return NR_OK;
+}
+
+int nr_sumsq_partials(const float* const* xs, const int64_t* ns, int nspan, float* partials, nr_stream_t stream) {
+    NR_REQUIRE(xs && ns && partials && nspan >= 1 && nspan <= kMaxAdamSpans,
+               "nr_sumsq_partials: bad arguments (1..%d spans)", kMaxAdamSpans);
+    SumsqSpans sp;
+    std::memset(&sp, 0, sizeof(sp));
+    sp.nspan = nspan;
+    for (int k = 0; k < nspan; ++k) {
+        NR_REQUIRE(ns[k] >= 0 && (xs[k] || ns[k] == 0), "nr_sumsq_partials: span %d: bad buffer", k);
+        sp.x[k] = xs[k];
+        sp.n[k] = ns[k];
+    }
+    hipLaunchKernelGGL(sumsq_spans_kernel, dim3(kSumsqBlocks), dim3(kSumsqThreads), 0,
+                       static_cast<hipStream_t>(stream), sp, partials);
+    NR_LAUNCH_CHECK("nr_sumsq_partials");
     return NR_OK;
 }
 

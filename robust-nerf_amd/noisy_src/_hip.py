@@ -43,6 +43,22 @@ class NrMlpConfig(ctypes.Structure):
     ]
 
 
+class NrAdamSpan(ctypes.Structure):
+    """Mirror of ``struct NrAdamSpan`` (include/nerf_hip.h)."""
+
+    _fields_ = [
+        ("params", c_vp),
+        ("grads", c_vp),
+        ("exp_avg", c_vp),
+        ("exp_avg_sq", c_vp),
+        ("n", c_i64),
+        ("sumsq_partials", c_vp),
+        ("max_norm", c_f),
+        ("pack_table", c_vp),
+        ("packed", c_vp),
+    ]
+
+
 NR_PREC_FP32 = 0
 NR_PREC_BF16 = 1
 NR_PREC_FP16 = 2
@@ -87,6 +103,10 @@ _SIGNATURES = {
     "nr_sumsq_workspace_bytes": (c_i64, []),
     "nr_sumsq": (c_i, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "nr_adam_step": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_d, c_d, c_d, c_d, c_i64, c_vp, c_f, c_vp]),
+    "nr_sumsq_partials": (c_i, [c_vp, c_vp, c_i, c_vp, c_vp]),
+    "nr_adam_multi": (c_i, [ctypes.POINTER(NrAdamSpan), c_i, c_d, c_d, c_d, c_d, c_i64, c_vp]),
+    "nr_mlp_pack_table_bytes": (c_i64, [_cfg_p]),
+    "nr_mlp_pack_table": (c_i, [_cfg_p, c_vp, c_vp]),
     "nr_expand_viewdirs": (c_i, [c_vp, c_i, c_i, c_vp, c_vp]),
     "nr_pts_bwd": (c_i, [c_vp, c_vp, c_i, c_i, c_vp, c_vp, c_vp]),
     "nr_viewdirs_bwd": (c_i, [c_vp, c_vp, c_i, c_i, c_vp, c_vp]),

@@ -17,6 +17,7 @@ fp32 (parity) or bf16 MFMA path.
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import List, Optional, Tuple
 
 import torch
@@ -140,6 +141,16 @@ def _check_supported(cfg: NrMlpConfig, config: ModelConfig, n_params: int) -> No
         raise RuntimeError(f"NeRF parameter layout mismatch: module {n_params} vs kernel plan {want}")
 
 
+# flat parameter buffer address -> the NeRF whose parameters it holds: FusedAdam
+# (optim.py) finds the network whose packed images a step may refresh in place
+_FLAT_OWNERS: "weakref.WeakValueDictionary[int, NeRF]" = weakref.WeakValueDictionary()
+
+
+def flat_owner(pflat: torch.Tensor):
+    """The NeRF whose flat parameter buffer starts at ``pflat`` (or None)."""
+    return _FLAT_OWNERS.get(pflat.data_ptr())
+
+
 class NeRF(nn.Module):
     """Reference model.py:83-196 (same submodules, parameter order and init)."""
 
@@ -179,6 +190,7 @@ class NeRF(nn.Module):
         self._flat: Optional[torch.Tensor] = None
         self._packed: Optional[torch.Tensor] = None
         self._packed_key = None
+        self._table: Optional[torch.Tensor] = None
         # called with the flat gradient as soon as the backward has produced it
         self._grad_ready_hook = None
 
@@ -205,6 +217,7 @@ class NeRF(nn.Module):
                     break
                 off += p.numel()
             if ok:
+                _FLAT_OWNERS[base] = self  # (again: e.g. after a deepcopy of the network)
                 return
         dev = params[0].device
         _hip.require_device(params[0])
@@ -218,6 +231,7 @@ class NeRF(nn.Module):
                 off += n
         self._flat = flat
         self._packed_key = None
+        _FLAT_OWNERS[flat.data_ptr()] = self
 
     def _packed_for_forward(self) -> torch.Tensor:
         params = self._param_list
@@ -231,6 +245,36 @@ class NeRF(nn.Module):
             call("nr_mlp_pack", cfg, ptr(self._flat), ptr(self._packed), _hip.stream_ptr())
             self._packed_key = key
         return self._packed
+
+    def _pack_table(self) -> torch.Tensor:
+        """The destination table of the packed images (nr_mlp_pack_table), built once per
+        device: where every flat parameter lands in them, for the fused optimizer step."""
+        t = self._table
+        if t is None or t.device != self._flat.device:
+            cfg = ctypes.byref(self._nr_cfg)
+            nbytes = int(_hip.load().nr_mlp_pack_table_bytes(cfg))
+            t = torch.empty(nbytes // 4, device=self._flat.device, dtype=torch.int32)
+            call("nr_mlp_pack_table", cfg, ptr(t), _hip.stream_ptr())
+            self._table = t
+        return t
+
+    def _fused_pack_target(self, pflat: torch.Tensor):
+        """(table, packed) when an optimizer step over ``pflat`` -- exactly this network's
+        flat parameters -- may refresh the packed images in its own launch (nr_adam_multi):
+        the images must be current for the parameters before the step.  Else None (the
+        next forward re-packs, as after any other change of the parameters)."""
+        flat, packed = self._flat, self._packed
+        if flat is None or packed is None or packed.device != flat.device:
+            return None
+        if pflat.data_ptr() != flat.data_ptr() or pflat.numel() != flat.numel():
+            return None
+        if self._packed_key != (flat.data_ptr(), tuple(p._version for p in self._param_list)):
+            return None
+        return self._pack_table(), packed
+
+    def _mark_packed_fresh(self) -> None:
+        """After a fused step refreshed the images: they match the new parameter versions."""
+        self._packed_key = (self._flat.data_ptr(), tuple(p._version for p in self._param_list))
 
     def forward(self, x: torch.Tensor, d: torch.Tensor | None = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """x (N,3) positions, d (N,3) view dirs -> rgb (N,3) in [0,1], sigma (N,1) >= 0."""

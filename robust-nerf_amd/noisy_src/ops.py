@@ -9,6 +9,7 @@ is no CPU or eager-torch fallback: CPU tensors raise.
 
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Tuple
 
 import torch
@@ -392,6 +393,42 @@ def sumsq_into(x: torch.Tensor, acc: torch.Tensor) -> None:
 def adam_step(p, g, m, v, lr, beta1, beta2, eps, step, sumsq=None, max_norm=1.0):
     call("nr_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr), float(beta1), float(beta2), float(eps),
          int(step), ptr(sumsq), float(max_norm), _stream())
+
+
+MAX_ADAM_SPANS = 8
+
+
+def sumsq_partials(xs, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The fixed-order partial sums of squares over the concatenation of the fp32 device
+    buffers ``xs`` (one clip group, <= 8 buffers): a (256,) device tensor that
+    ``adam_multi`` turns into the clip coefficient (no zeroed accumulator, one launch)."""
+    if not 1 <= len(xs) <= MAX_ADAM_SPANS:
+        raise ValueError(f"sumsq_partials: 1..{MAX_ADAM_SPANS} buffers, got {len(xs)}")
+    _check(*xs)
+    if out is None:
+        out = torch.empty(int(_hip.load().nr_sumsq_workspace_bytes()) // 4, device=xs[0].device, dtype=_f32)
+    ptrs = (ctypes.c_void_p * len(xs))(*[ptr(x) for x in xs])
+    ns = (ctypes.c_int64 * len(xs))(*[x.numel() for x in xs])
+    call("nr_sumsq_partials", ptrs, ns, len(xs), ptr(out), _stream())
+    return out
+
+
+def adam_multi(spans, lr, beta1, beta2, eps, step) -> None:
+    """torch.optim.Adam over up to 8 flat buffers in one launch.  Each span is a dict with
+    p, g, m, v (fp32 device buffers of one size), optional ``partials`` (the span's clip
+    group, from ``sumsq_partials``) and ``max_norm``, and optional ``table`` / ``packed``
+    (an MLP's destination table and images, refreshed in the same launch)."""
+    if not 1 <= len(spans) <= MAX_ADAM_SPANS:
+        raise ValueError(f"adam_multi: 1..{MAX_ADAM_SPANS} spans, got {len(spans)}")
+    arr = (_hip.NrAdamSpan * len(spans))()
+    for k, sp in enumerate(spans):
+        n = sp["p"].numel()
+        if any(sp[x].numel() != n for x in ("g", "m", "v")):
+            raise ValueError("adam_multi: p, g, m, v must have the same size")
+        arr[k] = _hip.NrAdamSpan(ptr(sp["p"]), ptr(sp["g"]), ptr(sp["m"]), ptr(sp["v"]), n,
+                                 ptr(sp.get("partials")), float(sp.get("max_norm", 1.0)),
+                                 ptr(sp.get("table")), ptr(sp.get("packed")))
+    call("nr_adam_multi", arr, len(spans), float(lr), float(beta1), float(beta2), float(eps), int(step), _stream())
 
 
 class _MSE(torch.autograd.Function):

@@ -85,7 +85,7 @@ class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, betas: Tuple[float, float] = (0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, amsgrad: bool = False, *, maximize: bool = False, foreach=None,
                  capturable: bool = False, differentiable: bool = False, fused=None,
-                 decoupled_weight_decay: bool = False):
+                 decoupled_weight_decay: bool = False, refresh_images: bool = True):
         # the reference's Adam (train.py:402, train_pose_opt.py:788-789) uses the defaults;
         # the fused kernel implements exactly that configuration
         if weight_decay != 0.0 or amsgrad or maximize or differentiable or decoupled_weight_decay:
@@ -96,6 +96,9 @@ class FusedAdam(torch.optim.Optimizer):
                                       maximize=False, foreach=foreach, capturable=capturable,
                                       differentiable=False, fused=fused, decoupled_weight_decay=False))
         self._flat_state = {}
+        # refresh a NeRF's packed MFMA images inside the Adam launch (False: the next
+        # forward re-packs them, the pre-fusion behaviour; tests compare the two)
+        self.refresh_images = refresh_images
 
     def load_state_dict(self, state_dict) -> None:
         """torch's load, then drop the flat m/v buffers so the next step adopts the loaded
@@ -128,19 +131,34 @@ class FusedAdam(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None, clip_groups=None):
+        """One Adam step of every parameter with a gradient; ``clip_groups`` folds
+        clip_grad_norm_ of each group into it.  The whole tail is one nr_sumsq_partials
+        launch per clip group and one nr_adam_multi launch per param group (up to 8
+        flat buffers each); a NeRF network's packed MFMA images are refreshed inside
+        that launch, so its next forward does not re-pack."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        clip_of = {}
-        if clip_groups:
-            for plist, max_norm in clip_groups:
-                plist = [p for p in plist if p.grad is not None]
-                if not plist:
-                    continue
+        from .model import flat_owner
+        clip_of, partials = {}, []
+        for plist, max_norm in clip_groups or ():
+            plist = [p for p in plist if p.grad is not None]
+            if not plist:
+                continue
+            flats = []
+            for run in _runs([p.grad for p in plist]):
+                flat = _contiguous_run(run)
+                if flat is None or flat.data_ptr() % 16:
+                    flat = torch.cat([g.reshape(-1) for g in run])
+                flats.append(flat)
+            if len(flats) > ops.MAX_ADAM_SPANS:  # one buffer per network in practice
                 acc = grad_sumsq(plist)
-                for p in plist:
-                    clip_of[id(p)] = (acc, float(max_norm))
+                flats = None
+            gi = len(partials)
+            partials.append(ops.sumsq_partials(flats) if flats is not None else acc)
+            for p in plist:
+                clip_of[id(p)] = (gi, float(max_norm), flats is not None)
         for group in self.param_groups:
             b1, b2 = group["betas"]
             params = [p for p in group["params"] if p.grad is not None]
@@ -149,20 +167,20 @@ class FusedAdam(torch.optim.Optimizer):
             for run in _runs(params):
                 cur = [run[0]]
                 for p in run[1:]:
-                    if clip_of.get(id(p), (None,))[0] is clip_of.get(id(cur[0]), (None,))[0]:
+                    if clip_of.get(id(p), (None,))[0] == clip_of.get(id(cur[0]), (None,))[0]:
                         cur.append(p)
                     else:
                         runs.append(cur)
                         cur = [p]
                 runs.append(cur)
+            by_step = {}
             for run in runs:
                 ops._check(run[0])
                 pflat = _contiguous_run(run)
                 if pflat is None or pflat.data_ptr() % 16:
                     raise RuntimeError("FusedAdam: parameters must be fp32 ROCm tensors (NeRF flat buffers)")
                 gflat = _contiguous_run([p.grad for p in run])
-                copy_back = gflat is None or gflat.data_ptr() % 16
-                if copy_back:
+                if gflat is None or gflat.data_ptr() % 16:
                     gflat = torch.cat([p.grad.reshape(-1) for p in run])
                 m, v = self._state_run(run)
                 st = self.state[run[0]]
@@ -170,9 +188,31 @@ class FusedAdam(torch.optim.Optimizer):
                 step = int(st["step"].item()) if st["step"].device.type == "cpu" else int(st["step"])
                 for p in run[1:]:
                     self.state[p]["step"] = st["step"]
-                sumsq, max_norm = clip_of.get(id(run[0]), (None, 1.0))
-                ops.adam_step(pflat, gflat, m, v, group["lr"], b1, b2, group["eps"], step, sumsq=sumsq,
-                              max_norm=max_norm)
-                for p in run:  # parameters changed behind autograd's back: bump versions (NeRF repacks)
-                    torch.autograd.graph.increment_version(p)
+                span = {"p": pflat, "g": gflat, "m": m, "v": v}
+                clip = clip_of.get(id(run[0]))
+                if clip is not None:
+                    gi, max_norm, is_partials = clip
+                    if is_partials:
+                        span["partials"], span["max_norm"] = partials[gi], max_norm
+                    else:  # a clip group of more than 8 buffers: the legacy accumulator path
+                        span["sumsq"], span["max_norm"] = partials[gi], max_norm
+                net = flat_owner(pflat) if ("sumsq" not in span and self.refresh_images) else None
+                target = net._fused_pack_target(pflat) if net is not None else None
+                if target is not None:
+                    span["table"], span["packed"] = target
+                by_step.setdefault(step, []).append((span, run, net if target is not None else None))
+            for step, items in by_step.items():
+                fused = [it for it in items if "sumsq" not in it[0]]
+                for k in range(0, len(fused), ops.MAX_ADAM_SPANS):
+                    ops.adam_multi([sp for sp, _, _ in fused[k:k + ops.MAX_ADAM_SPANS]], group["lr"], b1, b2,
+                                   group["eps"], step)
+                for sp, _, _ in items:
+                    if "sumsq" in sp:
+                        ops.adam_step(sp["p"], sp["g"], sp["m"], sp["v"], group["lr"], b1, b2, group["eps"], step,
+                                      sumsq=sp["sumsq"], max_norm=sp["max_norm"])
+                for _, run, net in items:
+                    for p in run:  # parameters changed behind autograd's back: bump versions
+                        torch.autograd.graph.increment_version(p)
+                    if net is not None:  # ... and its images were refreshed in the same launch
+                        net._mark_packed_fresh()
         return loss

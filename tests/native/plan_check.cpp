@@ -24,6 +24,11 @@ int main(int argc, char** argv) {
     for (int j = 0; j < p.n_jobs; ++j) {
         const DwJob& jb = p.job[j];
         printf("job %d NBz %d KB %d waves %d:", j, jb.NBz, jb.KB, jb.nwaves);
+        // the dW kernel stages at most dw_max_pieces 1-KB pieces per wave and tile
+        if ((jb.NBz + jb.KB) * p.fpb > kDwMaxWaves * dw_max_pieces(p.fpb == 2)) {
+            printf("\nstaging exceeds the per-wave pieces\n");
+            return 1;
+        }
         for (int v = 0; v < jb.nwaves; ++v) {
             const DwWave& w = jb.w[v];
             printf(" [%d+%d x %d+%d%s]", w.row0, w.np, w.col0, w.nq, w.bias ? " b" : "");

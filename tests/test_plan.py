@@ -24,7 +24,10 @@ def plan_check(tmp_path_factory):
 
 # pos_freqs dir_freqs n_layers skip_mask use_view_dirs precision
 CONFIGS = [(10, 4, 8, 1 << 4, 1, 1), (10, 4, 8, 1 << 4, 1, 0), (10, 4, 8, 1 << 4, 1, 2), (10, 4, 8, 1 << 4, 0, 1),
-           (6, 2, 4, 1 << 1, 1, 1), (10, 4, 12, (1 << 3) | (1 << 7), 1, 1), (4, 1, 1, 0, 1, 1)]
+           (6, 2, 4, 1 << 1, 1, 1), (10, 4, 12, (1 << 3) | (1 << 7), 1, 1), (4, 1, 1, 0, 1, 1),
+           # two and more skips: x-jobs of more than two dz layers exceed the dW staging
+           (10, 4, 7, (1 << 2) | (1 << 5), 1, 1), (10, 4, 7, (1 << 2) | (1 << 5), 1, 0),
+           (10, 4, 7, (1 << 2) | (1 << 5), 1, 2), (10, 4, 10, 0b10101010, 1, 1), (10, 4, 8, 0b100100, 1, 0)]
 
 
 @pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "-".join(map(str, c)))
@@ -32,3 +35,10 @@ def test_every_parameter_gradient_written_once(plan_check, cfg):
     r = subprocess.run([str(plan_check), *map(str, cfg)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "unwritten 0 doubly written 0" in r.stdout
+
+
+def test_too_many_dw_jobs_fails_cleanly(plan_check):
+    """16 layers with a skip after every one: more dW jobs than the kernel arguments
+    hold -- the plan refuses the config instead of overrunning its job table."""
+    r = subprocess.run([str(plan_check), "10", "4", "16", str((1 << 15) - 1), "1", "1"], capture_output=True, text=True)
+    assert r.returncode != 0 and "plan fail" in r.stdout, r.stdout

@@ -16,6 +16,7 @@ WRITE_SIZE counts 16-B streaming stores exactly.  Both count Infinity-Cache hits
 from __future__ import annotations
 
 import csv
+import hashlib
 import json
 import re
 import statistics
@@ -30,6 +31,18 @@ FAMILIES = {"mlp_fwd_kernel": "nr_mlp_forward", "mlp_bwd_kernel": "nr_mlp_backwa
             "mlp_fwd_rbm_kernel": "nr_mlp_forward", "mlp_bwd_rbm_kernel": "nr_mlp_backward_dx",
             "mlp_dinput_kernel": "nr_mlp_backward_dx (input grads)",
             "mlp_dw_kernel": "nr_mlp_backward_dw", "mlp_dw_reduce_kernel": "nr_mlp_backward_reduce"}
+
+
+def source_hash() -> str:
+    """sha1 over the HIP sources and the ABI header (bench.py computes the same hash, so
+    it uses a kernel summary only when it was profiled from the benchmarked sources)."""
+    h = hashlib.sha1()
+    files = sorted((ROOT / "robust-nerf_amd" / "csrc").glob("*")) + [ROOT / "include" / "nerf_hip.h"]
+    for f in files:
+        if f.suffix in (".hip", ".inc", ".hpp", ".h"):
+            h.update(f.name.encode())
+            h.update(f.read_bytes())
+    return h.hexdigest()[:12]
 
 
 def short(name: str) -> str:
@@ -70,12 +83,13 @@ def main(out_dir: str, tag: str, timed_steps: int = 0) -> None:
     with open(summ, "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["kernel", "precision", "grid_threads", "M_samples", "calls", "avg_ms", "median_ms", "total_ms",
-                    "timed_avg_ms"])
+                    "timed_avg_ms", "source_hash"])
+        sh = source_hash()
         for (k, g, M), v in sorted(rows.items(), key=lambda kv: -sum(kv[1])):
             timed = v[-timed_steps:] if (timed_steps and M and len(v) >= timed_steps) else []
             w.writerow([short(k), precision_of(k), g, M or "", len(v), f"{statistics.mean(v):.4f}",
                         f"{statistics.median(v):.4f}", f"{sum(v):.3f}",
-                        f"{statistics.mean(timed):.4f}" if timed else ""])
+                        f"{statistics.mean(timed):.4f}" if timed else "", sh])
     print(f"wrote {summ}")
 
     counters = defaultdict(lambda: defaultdict(list))
@@ -102,7 +116,8 @@ def main(out_dir: str, tag: str, timed_steps: int = 0) -> None:
         recs.append({"kernel": fam, "entry": FAMILIES[fam], "precision": precision_of(k), "M": M,
                      "fetch_size_bytes": fetch, "write_size_bytes": write,
                      "bytes_per_launch": 2.0 * fetch + write, "launches": len(c["FETCH_SIZE"])})
-    out = {"source": f"profiles/{tag}: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
+    out = {"source_hash": source_hash(),
+           "source": f"profiles/{tag}: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
                      "python bench.py --steps 2 --warmup 1 --no-cpu-baseline; traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (median)",
            "kernels": recs,
            # each (kernel, M) launches once per training step: the step's MLP HBM bytes
