@@ -419,6 +419,8 @@ def main():
                          "sliced over the ranks (default 0: weak scaling, --batch rays per GPU)")
     ap.add_argument("--cpu-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the training step as one captured hipGraph (engine.GraphedTrainer; N=1)")
     ap.add_argument("--pose-opt", action="store_true",
                     help="BASELINE cfg #3: joint pose optimisation step (train_pose_opt, poses optimising)")
     args = ap.parse_args()
@@ -513,6 +515,19 @@ def main():
     # dominant kernel = largest total time per step (no warm-up: time them all live)
     dom_key = max(wcalls, key=lambda k: wcalls[k][0] * wcalls[k][1]) if wcalls else None
 
+    if args.graph:
+        # one captured hipGraph per step: no Python runs inside the timed region, so the
+        # dominant kernel is timed over the eager warm-up steps above (and by rocprof)
+        from noisy_src.engine import GraphedTrainer
+        if world > 1 or args.pose_opt:
+            raise SystemExit("--graph: single-GPU Trainer steps only")
+        gtr = GraphedTrainer(trainer, *pool[0], warmup=2)
+
+        def step(k):  # noqa: F811
+            o, d, t = pool[k % len(pool)]
+            return gtr.step(o, d, t)
+        for k in range(3):
+            step(k)
     timer = _hip.CallTimer(mlp_entries, keys=[dom_key] if dom_key else None)
     _hip.set_timer(timer)
     if pg is not None:
@@ -539,7 +554,7 @@ def main():
 
     per_step = sorted(a.elapsed_time(b) for a, b in zip(evs, evs[1:]))
     step_pcts = [round(per_step[min(len(per_step) - 1, int(q * len(per_step)))], 4) for q in (0.1, 0.5, 0.9)]
-    calls = timer.summary()
+    calls = timer.summary() if not args.graph else {dom_key: wcalls[dom_key]}
     if dom_key is None:
         wcalls = calls
         dom_key = max(calls, key=lambda k: calls[k][0] * calls[k][1])
@@ -579,6 +594,7 @@ def main():
             "num_samples": rcfg.num_samples,
             "num_samples_fine": rcfg.num_samples_fine,
             "parallelism": f"dp{world}",
+            **({"execution": "hipGraph replay (engine.GraphedTrainer)"} if args.graph else {}),
         },
         "roofline": {
             "bound": bound,
@@ -590,6 +606,8 @@ def main():
             # one exists (reproducible from profiles/), else from the live launch time
             "frac": round((achieved * ms / rp_ms if rp_ms else achieved) / peak, 4),
             "frac_basis": (f"rocprof_ms: timed-region average of {rp_src} (same source_hash)" if rp_ms
+                           else "launch_ms: HIP events on the launching stream over the eager warm-up steps "
+                           "(a graph replay runs no Python)" if args.graph
                            else "launch_ms: live HIP events on the launching stream over the timed region"),
             "traffic": dom_traffic,
             "work_per_launch": work,

@@ -279,9 +279,13 @@ typedef struct NrAdamSpan {
     void* packed;
 } NrAdamSpan;
 /* torch.optim.Adam over nspan (<= 8) buffers of one param group (same lr and
- * 1-based step), one launch.                                                 */
+ * 1-based step), one launch.  sched (nullable, device): {lr / (1 - beta1^step),
+ * sqrt(1 - beta2^step)} as fp32, read by the kernel instead of the host lr/step,
+ * so a captured hipGraph of the step can be replayed with the schedule advanced
+ * by a 8-byte copy (lr / step then only validate).                          */
 int nr_adam_multi(const NrAdamSpan* spans, int nspan, double lr, double beta1,
-                  double beta2, double eps, int64_t step, nr_stream_t stream);
+                  double beta2, double eps, int64_t step, const float* sched,
+                  nr_stream_t stream);
 /* The destination table of an MLP's packed images for nr_adam_multi: for each
  * of the nr_mlp_param_count() flat parameters, 3 slots of (kind << 29 | byte
  * offset in packed), slot-major (table[s * n + i]); built once per config by

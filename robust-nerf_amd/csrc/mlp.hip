@@ -2224,6 +2224,7 @@ struct AdamSpanDev {
 struct AdamMultiArgs {
     AdamSpanDev s[kMaxAdamSpans];
     float omb1, b2, omb2, eps, step_size, bc2_sqrt;
+    const float* sched;  // nullable: {step_size, bc2_sqrt} read on the device (graph replay)
 };
 
 __device__ __forceinline__ void put_image(char* packed, uint32_t e, float p) {
@@ -2241,6 +2242,7 @@ __device__ __forceinline__ void put_image(char* packed, uint32_t e, float p) {
 __global__ void __launch_bounds__(kSumsqThreads) adam_multi_kernel(AdamMultiArgs a) {
     const AdamSpanDev& s = a.s[blockIdx.y];
     const float coef = s.partials ? clip_coef(block_sum_fixed(s.partials[threadIdx.x]), s.max_norm) : 1.0f;
+    const float step_size = a.sched ? a.sched[0] : a.step_size, bc2_sqrt = a.sched ? a.sched[1] : a.bc2_sqrt;
     const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
     const int64_t t0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const int64_t n = s.n;
@@ -2249,10 +2251,10 @@ __global__ void __launch_bounds__(kSumsqThreads) adam_multi_kernel(AdamMultiArgs
     for (int64_t i = t0; i < n4; i += stride) {
         float4 P = reinterpret_cast<float4*>(s.p)[i], G = reinterpret_cast<float4*>(s.g)[i];
         float4 M = reinterpret_cast<float4*>(s.m)[i], V = reinterpret_cast<float4*>(s.v)[i];
-        adam_one(P.x, G.x, M.x, V.x, coef, a.omb1, a.b2, a.omb2, a.step_size, a.bc2_sqrt, a.eps);
-        adam_one(P.y, G.y, M.y, V.y, coef, a.omb1, a.b2, a.omb2, a.step_size, a.bc2_sqrt, a.eps);
-        adam_one(P.z, G.z, M.z, V.z, coef, a.omb1, a.b2, a.omb2, a.step_size, a.bc2_sqrt, a.eps);
-        adam_one(P.w, G.w, M.w, V.w, coef, a.omb1, a.b2, a.omb2, a.step_size, a.bc2_sqrt, a.eps);
+        adam_one(P.x, G.x, M.x, V.x, coef, a.omb1, a.b2, a.omb2, step_size, bc2_sqrt, a.eps);
+        adam_one(P.y, G.y, M.y, V.y, coef, a.omb1, a.b2, a.omb2, step_size, bc2_sqrt, a.eps);
+        adam_one(P.z, G.z, M.z, V.z, coef, a.omb1, a.b2, a.omb2, step_size, bc2_sqrt, a.eps);
+        adam_one(P.w, G.w, M.w, V.w, coef, a.omb1, a.b2, a.omb2, step_size, bc2_sqrt, a.eps);
         reinterpret_cast<float4*>(s.p)[i] = P;
         reinterpret_cast<float4*>(s.g)[i] = G;
         reinterpret_cast<float4*>(s.m)[i] = M;
@@ -2270,7 +2272,7 @@ __global__ void __launch_bounds__(kSumsqThreads) adam_multi_kernel(AdamMultiArgs
     }
     for (int64_t i = 4 * n4 + t0; i < n; i += stride) {
         float P = s.p[i], G = s.g[i], M = s.m[i], V = s.v[i];
-        adam_one(P, G, M, V, coef, a.omb1, a.b2, a.omb2, a.step_size, a.bc2_sqrt, a.eps);
+        adam_one(P, G, M, V, coef, a.omb1, a.b2, a.omb2, step_size, bc2_sqrt, a.eps);
         s.p[i] = P;
         s.g[i] = G;
         s.m[i] = M;
@@ -2612,7 +2614,7 @@ int nr_mlp_pack_table(const NrMlpConfig* cfg, uint32_t* table, nr_stream_t strea
 }
 
 int nr_adam_multi(const NrAdamSpan* spans, int nspan, double lr, double b1, double b2, double eps, int64_t step,
-                  nr_stream_t stream) {
+                  const float* sched, nr_stream_t stream) {
     NR_REQUIRE(spans && nspan >= 1 && nspan <= kMaxAdamSpans && step >= 1,
                "nr_adam_multi: bad arguments (1..%d spans, step >= 1)", kMaxAdamSpans);
     AdamMultiArgs a;
@@ -2640,6 +2642,7 @@ int nr_adam_multi(const NrAdamSpan* spans, int nspan, double lr, double b1, doub
     a.eps = static_cast<float>(eps);
     a.step_size = static_cast<float>(lr / bc1);
     a.bc2_sqrt = static_cast<float>(std::sqrt(bc2));
+    a.sched = sched;
     const int grid = stream_grid(ceil_div_ll(nmax, 4), kSumsqThreads);
     hipLaunchKernelGGL(adam_multi_kernel, dim3(grid, nspan), dim3(kSumsqThreads), 0, static_cast<hipStream_t>(stream), a);
     NR_LAUNCH_CHECK("nr_adam_multi");

@@ -104,7 +104,7 @@ _SIGNATURES = {
     "nr_sumsq": (c_i, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "nr_adam_step": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_d, c_d, c_d, c_d, c_i64, c_vp, c_f, c_vp]),
     "nr_sumsq_partials": (c_i, [c_vp, c_vp, c_i, c_vp, c_vp]),
-    "nr_adam_multi": (c_i, [ctypes.POINTER(NrAdamSpan), c_i, c_d, c_d, c_d, c_d, c_i64, c_vp]),
+    "nr_adam_multi": (c_i, [ctypes.POINTER(NrAdamSpan), c_i, c_d, c_d, c_d, c_d, c_i64, c_vp, c_vp]),
     "nr_mlp_pack_table_bytes": (c_i64, [_cfg_p]),
     "nr_mlp_pack_table": (c_i, [_cfg_p, c_vp, c_vp]),
     "nr_expand_viewdirs": (c_i, [c_vp, c_i, c_i, c_vp, c_vp]),

@@ -165,6 +165,103 @@ class Trainer:
         return metrics
 
 
+class GraphedTrainer:
+    """``Trainer.step`` captured once into a hipGraph (``torch.cuda.graph``) and replayed:
+    the ~23 kernels of a step become one graph launch, so a step costs its GPU time even
+    where the host's Python dispatch (autograd, the optimizer's bookkeeping: ~1.3 ms per
+    step) exceeds it -- small per-GPU batches such as BASELINE cfg #4's 512 rays per rank.
+
+    Everything the replay needs is on the device: the rays go through static input
+    buffers, torch's graph-safe RNG draws the jitter / inverse-CDF uniforms (or the
+    caller passes them as static inputs), the fused Adam launch rewrites the packed
+    images, and the two step-dependent Adam scalars come from an 8-byte device pair
+    written before each replay (``FusedAdam.device_sched``); the LR schedule and the
+    optimizer's step counters advance on the host exactly as in ``Trainer.step``.
+    Single process: the data-parallel all-reduce is not captured."""
+
+    def __init__(self, trainer: "Trainer", rays_o: torch.Tensor, rays_d: torch.Tensor, target_rgb: torch.Tensor,
+                 t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None, warmup: int = 2):
+        if trainer.reducer is not None:
+            raise ValueError("GraphedTrainer: data-parallel trainers are not captured (use Trainer)")
+        self.trainer = trainer
+        opt = trainer.optimizer
+        if not isinstance(opt, FusedAdam) or len(opt.param_groups) != 1:
+            raise ValueError("GraphedTrainer needs the trainer's single-group FusedAdam")
+        self.static = [t.detach().clone() for t in (rays_o, rays_d, target_rgb)]
+        self.static_rand = [None if t is None else t.detach().clone() for t in (t_rand, u)]
+        dev = rays_o.device
+        self.sched = torch.zeros(2, device=dev, dtype=torch.float32)
+        # pinned staging ring for the per-step pair: a slot is rewritten only after the
+        # copy that read it has run (its event), however far the host runs ahead
+        self._ring = torch.zeros(64, 2, dtype=torch.float32).pin_memory()
+        self._ring_ev = [None] * 64
+        self._k = 0
+        # eager warm-up steps on a side stream (allocator pools, optimizer state, packed
+        # images and pack tables exist before the capture); they are real training steps
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                trainer.step(*self.static, *self.static_rand)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        # capture one step; its host-side bookkeeping (Adam step counters, LR scheduler)
+        # ran once without device work, so it is rolled back afterwards
+        steps = [(st, st["step"].clone()) for st in self._step_states()]
+        sched_state = trainer.scheduler.state_dict()
+        lr = [g["lr"] for g in opt.param_groups]
+        opt.device_sched = self.sched
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = trainer.step(*self.static, *self.static_rand)
+        for st, v in steps:
+            st["step"].copy_(v)
+        trainer.scheduler.load_state_dict(sched_state)
+        for g, v in zip(opt.param_groups, lr):
+            g["lr"] = v
+
+    def _step_states(self):
+        opt = self.trainer.optimizer
+        seen, out = set(), []
+        for p in opt.param_groups[0]["params"]:
+            st = opt.state.get(p)
+            if st and "step" in st and id(st["step"]) not in seen:
+                seen.add(id(st["step"]))
+                out.append(st)
+        return out
+
+    def step(self, rays_o: Optional[torch.Tensor] = None, rays_d: Optional[torch.Tensor] = None,
+             target_rgb: Optional[torch.Tensor] = None, t_rand: Optional[torch.Tensor] = None,
+             u: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+        """Replay one training step on these rays (copied into the static buffers; None:
+        the buffers as they are).  Returns the captured metrics (device tensors that every
+        replay overwrites)."""
+        for dst, src in zip(self.static + self.static_rand, (rays_o, rays_d, target_rgb, t_rand, u)):
+            if src is not None:
+                if dst is None:
+                    raise ValueError("GraphedTrainer: t_rand / u were drawn in the graph at capture")
+                dst.copy_(src)
+        opt = self.trainer.optimizer
+        group = opt.param_groups[0]
+        b1, b2 = group["betas"]
+        states = self._step_states()
+        nxt = int(states[0]["step"]) + 1
+        a, b = ops.adam_sched_values(group["lr"], b1, b2, nxt)
+        slot = self._k % len(self._ring_ev)
+        if self._ring_ev[slot] is not None:
+            self._ring_ev[slot].synchronize()
+        self._ring[slot, 0], self._ring[slot, 1] = a, b  # fp32 rounding, as the host path's
+        self.sched.copy_(self._ring[slot], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ring_ev[slot] = ev
+        self._k += 1
+        self.graph.replay()
+        for st in states:
+            st["step"] += 1
+        self.trainer.scheduler.step()
+        return self.out
+
+
 class PoseTrainer:
     """The joint pose-optimisation step without host synchronisation (BASELINE cfg #3).
 

@@ -413,11 +413,19 @@ def sumsq_partials(xs, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     return out
 
 
-def adam_multi(spans, lr, beta1, beta2, eps, step) -> None:
+def adam_sched_values(lr: float, beta1: float, beta2: float, step: int) -> Tuple[float, float]:
+    """(lr / (1 - beta1^step), sqrt(1 - beta2^step)): the two step-dependent Adam scalars,
+    in double as nr_adam_step / torch's Adam compute them (to be rounded to fp32)."""
+    import math
+    return lr / (1.0 - beta1 ** step), math.sqrt(1.0 - beta2 ** step)
+
+
+def adam_multi(spans, lr, beta1, beta2, eps, step, sched: Optional[torch.Tensor] = None) -> None:
     """torch.optim.Adam over up to 8 flat buffers in one launch.  Each span is a dict with
     p, g, m, v (fp32 device buffers of one size), optional ``partials`` (the span's clip
     group, from ``sumsq_partials``) and ``max_norm``, and optional ``table`` / ``packed``
-    (an MLP's destination table and images, refreshed in the same launch)."""
+    (an MLP's destination table and images, refreshed in the same launch).  ``sched``:
+    a device fp32 pair (``adam_sched_values``) the kernel reads instead of lr / step."""
     if not 1 <= len(spans) <= MAX_ADAM_SPANS:
         raise ValueError(f"adam_multi: 1..{MAX_ADAM_SPANS} spans, got {len(spans)}")
     arr = (_hip.NrAdamSpan * len(spans))()
@@ -428,7 +436,8 @@ def adam_multi(spans, lr, beta1, beta2, eps, step) -> None:
         arr[k] = _hip.NrAdamSpan(ptr(sp["p"]), ptr(sp["g"]), ptr(sp["m"]), ptr(sp["v"]), n,
                                  ptr(sp.get("partials")), float(sp.get("max_norm", 1.0)),
                                  ptr(sp.get("table")), ptr(sp.get("packed")))
-    call("nr_adam_multi", arr, len(spans), float(lr), float(beta1), float(beta2), float(eps), int(step), _stream())
+    call("nr_adam_multi", arr, len(spans), float(lr), float(beta1), float(beta2), float(eps), int(step), ptr(sched),
+         _stream())
 
 
 class _MSE(torch.autograd.Function):

@@ -99,6 +99,9 @@ class FusedAdam(torch.optim.Optimizer):
         # refresh a NeRF's packed MFMA images inside the Adam launch (False: the next
         # forward re-packs them, the pre-fusion behaviour; tests compare the two)
         self.refresh_images = refresh_images
+        # graph mode (engine.GraphedTrainer): a device fp32 pair {lr/bc1, sqrt(bc2)} the
+        # Adam launch reads, so a captured step replays with the schedule advanced
+        self.device_sched: Optional[torch.Tensor] = None
 
     def load_state_dict(self, state_dict) -> None:
         """torch's load, then drop the flat m/v buffers so the next step adopts the loaded
@@ -205,7 +208,7 @@ class FusedAdam(torch.optim.Optimizer):
                 fused = [it for it in items if "sumsq" not in it[0]]
                 for k in range(0, len(fused), ops.MAX_ADAM_SPANS):
                     ops.adam_multi([sp for sp, _, _ in fused[k:k + ops.MAX_ADAM_SPANS]], group["lr"], b1, b2,
-                                   group["eps"], step)
+                                   group["eps"], step, sched=self.device_sched)
                 for sp, _, _ in items:
                     if "sumsq" in sp:
                         ops.adam_step(sp["p"], sp["g"], sp["m"], sp["v"], group["lr"], b1, b2, group["eps"], step,

@@ -138,3 +138,45 @@ def test_trainer_fused_tail_equals_adam_then_repack(precision):
         assert torch.equal(na.flat_params(), nb.flat_params())
         assert torch.equal(na._packed, _fresh_pack(na))
         assert torch.equal(nb._packed_for_forward(), _fresh_pack(nb))
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_graphed_trainer_equals_eager_trainer(precision):
+    """engine.GraphedTrainer (the step captured once into a hipGraph and replayed, the
+    Adam schedule advanced through its device pair) performs exactly the eager
+    Trainer's steps: bit-identical losses, parameters, packed images, LR and Adam step
+    counters, with the randoms injected through the static inputs."""
+    from noisy_src.config import ModelConfig, RenderConfig
+    from noisy_src.engine import GraphedTrainer, Trainer
+    from noisy_src.model import create_nerf
+    rc = RenderConfig(num_samples=32, num_samples_fine=32)
+    trainers = []
+    for _ in range(2):
+        torch.manual_seed(17)
+        mc, mf = create_nerf(ModelConfig(precision=precision))
+        trainers.append(Trainer(mc.to(DEV), mf.to(DEV), rc))
+    eager, tr_g = trainers
+    g = torch.Generator().manual_seed(23)
+    B = 256
+
+    def batch():
+        o = torch.randn(B, 3, generator=g) * 0.1 + torch.tensor([0.0, 0.0, 4.0])
+        dd = torch.nn.functional.normalize(torch.randn(B, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, -1.0]), dim=-1)
+        return [t.to(DEV) for t in (o, dd, torch.rand(B, 3, generator=g), torch.rand(B, rc.num_samples, generator=g),
+                                    torch.rand(B, rc.num_samples_fine, generator=g))]
+
+    b0 = batch()
+    graphed = GraphedTrainer(tr_g, *b0, warmup=2)
+    for _ in range(2):
+        eager.step(*b0)
+    for k in range(5):
+        bk = batch()
+        le = float(eager.step(*bk)["loss"])
+        lg = float(graphed.step(*bk)["loss"])
+        assert le == lg, (k, le, lg)
+    for na, nb in ((eager.model_coarse, tr_g.model_coarse), (eager.model_fine, tr_g.model_fine)):
+        assert torch.equal(na.flat_params(), nb.flat_params())
+        assert torch.equal(nb._packed, _fresh_pack(nb))
+    assert eager.optimizer.param_groups[0]["lr"] == tr_g.optimizer.param_groups[0]["lr"]
+    pe, pg = eager.params[0], tr_g.params[0]
+    assert int(eager.optimizer.state[pe]["step"]) == int(tr_g.optimizer.state[pg]["step"]) == 7
