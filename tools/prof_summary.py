@@ -55,36 +55,11 @@ def precision_of(name: str) -> str:
     return {"1": "bf16", "0": "fp32", "2": "fp16"}.get(m.group(1), "") if m else ""
 
 
-# Persistent kernels (one workgroup per CU) do not reveal M in their grid: their launches
-# cycle through the training step's M values in dispatch order (bench.py: coarse then
-# fine forward, fine then coarse backward), set by NR_PROF_M="<Mc>,<Mf>" (default cfg #2).
-PERSISTENT = {"mlp_fwd_rbm_kernel": 0, "mlp_bwd_rbm_kernel": 1}
-
-
-class _Cycle:
-    def __init__(self):
-        import os
-        mc, mf = (int(v) for v in os.environ.get("NR_PROF_M", "262144,786432").split(","))
-        self.seq = {0: [mc, mf], 1: [mf, mc]}
-        self.k = {0: 0, 1: 0}
-
-    def next(self, which: int) -> int:
-        v = self.seq[which][self.k[which] % 2]
-        self.k[which] += 1
-        return v
-
-
-_cycle = None
-
-
 def sample_count(name: str, grid: int, last_M: int) -> int:
-    """M of a fused-MLP launch: the chunk-major forward/backward kernels run one 32-sample
-    tile per wave; the persistent row-block-major ones follow the step's M cycle; dW and
-    its reduction follow the backward launch of the same M in the stream."""
+    """M of a fused-MLP launch: the forward/backward kernels run one 32-sample tile per
+    wave; dW and its reduction follow the backward launch of the same M in the stream."""
     fam = short(name)
-    if fam in PERSISTENT:
-        return _cycle.next(PERSISTENT[fam])
-    if fam in ("mlp_fwd_kernel", "mlp_bwd_kernel"):
+    if fam in ("mlp_fwd_kernel", "mlp_bwd_kernel", "mlp_fwd_rbm_kernel", "mlp_bwd_rbm_kernel"):
         return grid // 64 * 32
     if fam in ("mlp_dw_kernel", "mlp_dw_reduce_kernel", "mlp_dinput_kernel"):
         return last_M
@@ -94,10 +69,8 @@ def sample_count(name: str, grid: int, last_M: int) -> int:
 def main(out_dir: str, tag: str, timed_steps: int = 0) -> None:
     """``timed_steps`` K: also average each fused-MLP key over its last K launches, the
     launches of bench.py's timed region (each key launches once per step)."""
-    global _cycle
     base = Path(out_dir)
     rows = defaultdict(list)
-    _cycle = _Cycle()
     with open(base / "prof" / "run_kernel_trace.csv") as f:
         trace = sorted(csv.DictReader(f), key=lambda r: int(r["Dispatch_Id"]))
     last_M = 0
@@ -121,7 +94,6 @@ def main(out_dir: str, tag: str, timed_steps: int = 0) -> None:
 
     counters = defaultdict(lambda: defaultdict(list))
     for sub, cname in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
-        _cycle = _Cycle()
         p = base / sub / "run_counter_collection.csv"
         if not p.exists():
             continue
