@@ -152,7 +152,14 @@ def last_error() -> str:
     return msg.decode() if msg else ""
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device: Optional[torch.device] = None) -> int:
+    """The current HIP stream of ``device`` (default: the current device) as an int --
+    the raw accessor, without building a torch.cuda.Stream object per launch."""
+    if _raw_stream is not None and device is None:
+        return _raw_stream(torch.cuda.current_device())
     return torch.cuda.current_stream(device).cuda_stream
 
 

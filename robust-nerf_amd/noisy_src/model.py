@@ -70,7 +70,7 @@ class _MLPFunction(torch.autograd.Function):
     def forward(ctx, x, d, net, *params):
         cfg = ctypes.byref(net._nr_cfg)
         flat = net._flat
-        packed = net._packed_for_forward()
+        packed = net._packed_for_forward(params)
         xc = ops._c(x)
         dc = ops._c(d) if d is not None else None
         M = xc.shape[0]
@@ -86,6 +86,7 @@ class _MLPFunction(torch.autograd.Function):
             ctx.save_for_backward(xc, dc if dc is not None else xc.new_empty(0), rgb, sigma)
             ctx.has_d = dc is not None
             ctx.keep = (net, saved, packed, flat)
+            ctx.shapes = [p.shape for p in params]
         return rgb, sigma
 
     @staticmethod
@@ -109,15 +110,16 @@ class _MLPFunction(torch.autograd.Function):
             call("nr_mlp_backward_reduce", cfg, M, ptr(ws), ptr(gflat), st, tag=tag)
         else:
             gflat.zero_()
+        net._last_gflat = gflat  # FusedAdam's fast path reads the flat gradient directly
         if net._grad_ready_hook is not None:
             # data parallel: start this net's gradient all-reduce now, overlapping the
             # rest of the backward (the fine net finishes before the coarse one)
             net._grad_ready_hook(gflat)
         grads = []
         off = 0
-        for p in net._param_list:
-            n = p.numel()
-            grads.append(gflat[off:off + n].view(p.shape))
+        for shape in ctx.shapes:
+            n = shape.numel()
+            grads.append(gflat[off:off + n].view(shape))
             off += n
         return (g_x, g_d, None, *grads)
 
@@ -191,6 +193,7 @@ class NeRF(nn.Module):
         self._packed: Optional[torch.Tensor] = None
         self._packed_key = None
         self._table: Optional[torch.Tensor] = None
+        self._last_gflat: Optional[torch.Tensor] = None  # the last backward's flat gradient
         # called with the flat gradient as soon as the backward has produced it
         self._grad_ready_hook = None
 
@@ -204,8 +207,8 @@ class NeRF(nn.Module):
         self._ensure_flat()
         return self._flat
 
-    def _ensure_flat(self) -> None:
-        params = self._param_list
+    def _ensure_flat(self, params: Optional[List[nn.Parameter]] = None) -> None:
+        params = self._param_list if params is None else params
         flat = self._flat
         if flat is not None and flat.device == params[0].device:
             off = 0
@@ -233,8 +236,8 @@ class NeRF(nn.Module):
         self._packed_key = None
         _FLAT_OWNERS[flat.data_ptr()] = self
 
-    def _packed_for_forward(self) -> torch.Tensor:
-        params = self._param_list
+    def _packed_for_forward(self, params: Optional[List[nn.Parameter]] = None) -> torch.Tensor:
+        params = self._param_list if params is None else params
         key = (self._flat.data_ptr(), tuple(p._version for p in params))
         if self._packed is None or self._packed_key != key or self._packed.device != self._flat.device:
             cfg = ctypes.byref(self._nr_cfg)
@@ -258,7 +261,7 @@ class NeRF(nn.Module):
             self._table = t
         return t
 
-    def _fused_pack_target(self, pflat: torch.Tensor):
+    def _fused_pack_target(self, pflat: torch.Tensor, params: Optional[List[nn.Parameter]] = None):
         """(table, packed) when an optimizer step over ``pflat`` -- exactly this network's
         flat parameters -- may refresh the packed images in its own launch (nr_adam_multi):
         the images must be current for the parameters before the step.  Else None (the
@@ -268,13 +271,15 @@ class NeRF(nn.Module):
             return None
         if pflat.data_ptr() != flat.data_ptr() or pflat.numel() != flat.numel():
             return None
-        if self._packed_key != (flat.data_ptr(), tuple(p._version for p in self._param_list)):
+        params = self._param_list if params is None else params
+        if self._packed_key != (flat.data_ptr(), tuple(p._version for p in params)):
             return None
         return self._pack_table(), packed
 
-    def _mark_packed_fresh(self) -> None:
+    def _mark_packed_fresh(self, params: Optional[List[nn.Parameter]] = None) -> None:
         """After a fused step refreshed the images: they match the new parameter versions."""
-        self._packed_key = (self._flat.data_ptr(), tuple(p._version for p in self._param_list))
+        params = self._param_list if params is None else params
+        self._packed_key = (self._flat.data_ptr(), tuple(p._version for p in params))
 
     def forward(self, x: torch.Tensor, d: torch.Tensor | None = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """x (N,3) positions, d (N,3) view dirs -> rgb (N,3) in [0,1], sigma (N,1) >= 0."""
@@ -282,8 +287,9 @@ class NeRF(nn.Module):
         if self.config.use_view_dirs and d is None:
             # reference model.py:187-193 would feed 256 features to a 283-input layer
             raise ValueError("NeRF with use_view_dirs=True needs view directions d")
-        self._ensure_flat()
-        return _MLPFunction.apply(x, d if self.config.use_view_dirs else None, self, *self._param_list)
+        params = self._param_list
+        self._ensure_flat(params)
+        return _MLPFunction.apply(x, d if self.config.use_view_dirs else None, self, *params)
 
 
 def create_nerf(config: ModelConfig | None = None) -> Tuple[NeRF, NeRF | None]:

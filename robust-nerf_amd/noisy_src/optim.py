@@ -102,6 +102,9 @@ class FusedAdam(torch.optim.Optimizer):
         # graph mode (engine.GraphedTrainer): a device fp32 pair {lr/bc1, sqrt(bc2)} the
         # Adam launch reads, so a captured step replays with the schedule advanced
         self.device_sched: Optional[torch.Tensor] = None
+        # parameter lists that are whole NeRF networks, by the parameters' identities:
+        # [(net, start, end)] (False: not such a list) -- the per-step fast path
+        self._nerf_plans = {}
 
     def load_state_dict(self, state_dict) -> None:
         """torch's load, then drop the flat m/v buffers so the next step adopts the loaded
@@ -132,6 +135,46 @@ class FusedAdam(torch.optim.Optimizer):
         self._flat_state[key] = (m, v)
         return m, v
 
+    def _nerf_runs(self, params: List[torch.Tensor]):
+        """[(run, pflat, gflat, net)] when ``params`` is a concatenation of whole NeRF
+        networks' parameter lists (in their order) whose gradients are the views of the
+        network's last backward's flat gradient: each network's flat parameter and
+        gradient buffers, with O(parameters) pointer checks instead of rebuilding the
+        runs (the generic path costs ~1 ms of host time per step).  None otherwise."""
+        from .model import flat_owner
+        key = tuple(map(id, params))
+        plan = self._nerf_plans.get(key)
+        if plan is None:
+            plan, i = [], 0
+            while i < len(params):
+                net = flat_owner(params[i])
+                plist = net._param_list if net is not None else None
+                if (not plist or len(params) - i < len(plist)
+                        or any(a is not b for a, b in zip(params[i:i + len(plist)], plist))):
+                    plan = False
+                    break
+                offs, off = [], 0
+                for p in plist:
+                    offs.append(off)
+                    off += p.numel()
+                plan.append((net, i, i + len(plist), offs))
+                i += len(plist)
+            self._nerf_plans[key] = plan
+        if not plan:
+            return None
+        out = []
+        for net, i0, i1, offs in plan:
+            run = params[i0:i1]
+            flat, g = net._flat, net._last_gflat
+            if flat is None or g is None or run[0].data_ptr() != flat.data_ptr() or g.numel() != flat.numel():
+                return None
+            gp = g.data_ptr()
+            for p, off in zip(run, offs):
+                if p.grad is None or p.grad.data_ptr() != gp + 4 * off or p.data_ptr() != flat.data_ptr() + 4 * off:
+                    return None
+            out.append((run, flat, g, net))
+        return out
+
     @torch.no_grad()
     def step(self, closure=None, clip_groups=None):
         """One Adam step of every parameter with a gradient; ``clip_groups`` folds
@@ -149,12 +192,16 @@ class FusedAdam(torch.optim.Optimizer):
             plist = [p for p in plist if p.grad is not None]
             if not plist:
                 continue
-            flats = []
-            for run in _runs([p.grad for p in plist]):
-                flat = _contiguous_run(run)
-                if flat is None or flat.data_ptr() % 16:
-                    flat = torch.cat([g.reshape(-1) for g in run])
-                flats.append(flat)
+            fast = self._nerf_runs(plist)
+            if fast is not None:
+                flats = [g for _, _, g, _ in fast]
+            else:
+                flats = []
+                for run in _runs([p.grad for p in plist]):
+                    flat = _contiguous_run(run)
+                    if flat is None or flat.data_ptr() % 16:
+                        flat = torch.cat([g.reshape(-1) for g in run])
+                    flats.append(flat)
             if len(flats) > ops.MAX_ADAM_SPANS:  # one buffer per network in practice
                 acc = grad_sumsq(plist)
                 flats = None
@@ -166,25 +213,33 @@ class FusedAdam(torch.optim.Optimizer):
             b1, b2 = group["betas"]
             params = [p for p in group["params"] if p.grad is not None]
             # runs must agree on memory layout AND on the clip group
-            runs = []
-            for run in _runs(params):
-                cur = [run[0]]
-                for p in run[1:]:
-                    if clip_of.get(id(p), (None,))[0] == clip_of.get(id(cur[0]), (None,))[0]:
-                        cur.append(p)
-                    else:
-                        runs.append(cur)
-                        cur = [p]
-                runs.append(cur)
+            fast = self._nerf_runs(params)
+            if fast is not None and any(len({clip_of.get(id(p), (None,))[0] for p in run}) != 1
+                                        for run, _, _, _ in fast):
+                fast = None
+            if fast is not None:
+                runs = [(run, pflat, gflat) for run, pflat, gflat, _ in fast]
+            else:
+                runs = []
+                for run in _runs(params):
+                    cur = [run[0]]
+                    for p in run[1:]:
+                        if clip_of.get(id(p), (None,))[0] == clip_of.get(id(cur[0]), (None,))[0]:
+                            cur.append(p)
+                        else:
+                            runs.append((cur, None, None))
+                            cur = [p]
+                    runs.append((cur, None, None))
             by_step = {}
-            for run in runs:
-                ops._check(run[0])
-                pflat = _contiguous_run(run)
-                if pflat is None or pflat.data_ptr() % 16:
-                    raise RuntimeError("FusedAdam: parameters must be fp32 ROCm tensors (NeRF flat buffers)")
-                gflat = _contiguous_run([p.grad for p in run])
-                if gflat is None or gflat.data_ptr() % 16:
-                    gflat = torch.cat([p.grad.reshape(-1) for p in run])
+            for run, pflat, gflat in runs:
+                if pflat is None:
+                    ops._check(run[0])
+                    pflat = _contiguous_run(run)
+                    if pflat is None or pflat.data_ptr() % 16:
+                        raise RuntimeError("FusedAdam: parameters must be fp32 ROCm tensors (NeRF flat buffers)")
+                    gflat = _contiguous_run([p.grad for p in run])
+                    if gflat is None or gflat.data_ptr() % 16:
+                        gflat = torch.cat([p.grad.reshape(-1) for p in run])
                 m, v = self._state_run(run)
                 st = self.state[run[0]]
                 st["step"] += 1
@@ -200,7 +255,7 @@ class FusedAdam(torch.optim.Optimizer):
                     else:  # a clip group of more than 8 buffers: the legacy accumulator path
                         span["sumsq"], span["max_norm"] = partials[gi], max_norm
                 net = flat_owner(pflat) if ("sumsq" not in span and self.refresh_images) else None
-                target = net._fused_pack_target(pflat) if net is not None else None
+                target = net._fused_pack_target(pflat, run) if net is not None else None
                 if target is not None:
                     span["table"], span["packed"] = target
                 by_step.setdefault(step, []).append((span, run, net if target is not None else None))
@@ -217,5 +272,5 @@ class FusedAdam(torch.optim.Optimizer):
                     for p in run:  # parameters changed behind autograd's back: bump versions
                         torch.autograd.graph.increment_version(p)
                     if net is not None:  # ... and its images were refreshed in the same launch
-                        net._mark_packed_fresh()
+                        net._mark_packed_fresh(run)
         return loss

@@ -138,6 +138,11 @@ def test_trainer_fused_tail_equals_adam_then_repack(precision):
         assert torch.equal(na.flat_params(), nb.flat_params())
         assert torch.equal(na._packed, _fresh_pack(na))
         assert torch.equal(nb._packed_for_forward(), _fresh_pack(nb))
+    # both took the whole-network fast path (flat buffers straight from the networks)
+    for tr in trainers:
+        plans = list(tr.optimizer._nerf_plans.values())
+        assert plans and all(plans) and len(plans[0]) == 2
+        assert tr.optimizer._nerf_runs(tr.params) is not None
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
