@@ -75,6 +75,41 @@ def mean_over_ranks(values, process_group=None):
     return t
 
 
+class LaggedScalars:
+    """Logged device scalars read back one iteration late.  ``push`` queues a pinned copy
+    of this iteration's values and returns the previous iteration's (synchronising on its
+    event only), so the host queues step i+1 while step i still runs instead of idling on
+    a per-step ``.item()``/``.tolist()`` as the reference's loops do (train.py:386-420).
+    ``flush`` returns the pending values now (before a validation / checkpoint)."""
+
+    def __init__(self, n_max: int = 8):
+        self._buf = [torch.zeros(n_max, dtype=torch.float32, pin_memory=True) for _ in range(2)]
+        self._k = 0
+        self._pending = None
+
+    def push(self, values: torch.Tensor, meta=None):
+        n = values.numel()
+        host = self._buf[self._k % 2]  # the slot's previous values were resolved by the last push
+        self._k += 1
+        host[:n].copy_(values.reshape(-1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        prev, self._pending = self._pending, (host, n, ev, meta)
+        return self._resolve(prev)
+
+    def flush(self):
+        prev, self._pending = self._pending, None
+        return self._resolve(prev)
+
+    @staticmethod
+    def _resolve(p):
+        if p is None:
+            return None
+        host, n, ev, meta = p
+        ev.synchronize()
+        return host[:n].tolist(), meta
+
+
 def lr_lambda_factory(lr_decay: int):
     decay_steps = lr_decay * 1000
 
@@ -197,11 +232,15 @@ class GraphedTrainer:
         self._ring_ev = [None] * 64
         self._k = 0
         # eager warm-up steps on a side stream (allocator pools, optimizer state, packed
-        # images and pack tables exist before the capture); they are real training steps
+        # images and pack tables exist before the capture); they are real training steps.
+        # warmup=0 is accepted once the trainer has stepped eagerly (the state exists):
+        # the capture then trains on nothing, so a caller's step sequence is unchanged
+        if warmup < 1 and not self._step_states():
+            warmup = 1
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
-            for _ in range(max(1, warmup)):
+            for _ in range(warmup):
                 trainer.step(*self.static, *self.static_rand)
         torch.cuda.current_stream(dev).wait_stream(side)
         # capture one step; its host-side bookkeeping (Adam step counters, LR scheduler)
@@ -218,6 +257,9 @@ class GraphedTrainer:
         trainer.scheduler.load_state_dict(sched_state)
         for g, v in zip(opt.param_groups, lr):
             g["lr"] = v
+        # the graph holds the pair's address; eager steps between replays (a batch of
+        # another shape, see train.train) use the host scalars again
+        opt.device_sched = None
 
     def _step_states(self):
         opt = self.trainer.optimizer
@@ -234,7 +276,7 @@ class GraphedTrainer:
              u: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         """Replay one training step on these rays (copied into the static buffers; None:
         the buffers as they are).  Returns the captured metrics (device tensors that every
-        replay overwrites)."""
+        replay overwrites).  Eager ``trainer.step`` calls may be interleaved (same state)."""
         for dst, src in zip(self.static + self.static_rand, (rays_o, rays_d, target_rgb, t_rand, u)):
             if src is not None:
                 if dst is None:

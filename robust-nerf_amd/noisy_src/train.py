@@ -38,7 +38,7 @@ import torch
 from . import ops
 from .config import NeRFConfig
 from .data import BlenderData, RayDataset, RaySampler, create_data_loaders
-from .engine import Trainer, check_run_args, init_distributed, mean_over_ranks, rank_slice
+from .engine import GraphedTrainer, LaggedScalars, Trainer, check_run_args, init_distributed, mean_over_ranks, rank_slice
 from .logger import ExperimentLogger, TrainingMetrics, ValidationMetrics
 from .metrics import LPIPSMetric, compute_mse, compute_psnr, compute_ssim
 from .model import create_nerf
@@ -187,16 +187,20 @@ def load_checkpoint(checkpoint_path, model_coarse, model_fine, optimizer: Option
 
 def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
           train_data: Optional[BlenderData] = None, val_data: Optional[BlenderData] = None,
-          process_group=None, log=print) -> Dict[str, object]:
+          process_group=None, log=print, graph: bool = False) -> Dict[str, object]:
     """Reference train.py:307-577.  ``train_data`` / ``val_data`` (optional) replace the
     on-disk scene; ``process_group`` (or a torchrun environment, see ``main``) makes it
-    data parallel.  Returns the networks, the output directory and the final metrics."""
+    data parallel.  ``graph`` (one process only) replays the training step from a hipGraph
+    after the first iteration (``engine.GraphedTrainer``; same results as eager).
+    Returns the networks, the output directory and the final metrics."""
     import torch.distributed as dist
 
     rank, world = 0, 1
     if process_group is not None:
         rank, world = dist.get_rank(process_group), dist.get_world_size(process_group)
     check_run_args(config, world, train_data, val_data)
+    if graph and world > 1:
+        raise ValueError("train(graph=True) is single-process: the data-parallel all-reduce is not captured")
     set_seed(config.train.seed)
     device = config.train.device
     if device.startswith("cuda") and not torch.cuda.is_available():
@@ -248,6 +252,24 @@ def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
     start = time.time()
     best_psnr = 0.0
     iteration = 0
+    graphed = None
+    lagged = LaggedScalars()  # logged losses read one iteration late: no per-step host sync
+    t_prev = time.time()
+
+    def log_iteration(done):
+        if done is None or logger is None:
+            return
+        vals, (it, keys, lr, batch_time) = done
+        vm = dict(zip(keys, vals))
+        last = vm.get("loss_fine", vm["loss_coarse"])
+        psnr = -10.0 * math.log10(last) if last > 0 else float("inf")
+        logger.log_training(TrainingMetrics(iteration=it, loss=vm["loss"], loss_coarse=vm["loss_coarse"],
+                                            loss_fine=vm.get("loss_fine"), psnr=psnr, learning_rate=lr,
+                                            time_per_iter=batch_time, rays_per_sec=B / batch_time))
+        if it % config.train.log_every == 0:
+            log(f"[{it:7d}/{config.train.num_iterations}] loss: {vm['loss']:.5f} | psnr: {psnr:.2f} | "
+                f"lr: {lr:.2e} | rays/s: {B / batch_time:.0f} | time: {(time.time() - start) / 60:.1f}min")
+
     while iteration < config.train.num_iterations:
         for batch in sampler:
             if iteration >= config.train.num_iterations:
@@ -262,24 +284,24 @@ def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
             t_rand = torch.rand(n, rc.num_samples, device=device) if rc.perturb else None
             u = torch.rand(n, rc.num_samples_fine, device=device) if (rc.use_hierarchical and model_fine) else None
             sl = rank_slice(n, rank, world) if world > 1 else slice(0, n)
-            t0 = time.time()
-            m = trainer.step(batch["rays_o"][sl], batch["rays_d"][sl], batch["target_rgb"][sl],
-                             t_rand=None if t_rand is None else t_rand[sl], u=None if u is None else u[sl])
+            args = (batch["rays_o"][sl], batch["rays_d"][sl], batch["target_rgb"][sl],
+                    None if t_rand is None else t_rand[sl], None if u is None else u[sl])
+            if graph and graphed is None and iteration >= 1:
+                # captured after one eager step (state exists), on this batch's shape
+                graphed = GraphedTrainer(trainer, *args, warmup=0)
+            if graphed is not None and args[0].shape == graphed.static[0].shape:
+                m = graphed.step(*args)
+            else:  # eager (also an epoch's short final batch in graph mode)
+                m = trainer.step(*args)
             keys = ["loss", "loss_coarse"] + (["loss_fine"] if "loss_fine" in m else [])
-            vals = mean_over_ranks([m[k] for k in keys], process_group).tolist()
-            batch_time = time.time() - t0
-            vm = dict(zip(keys, vals))
-            last = vm.get("loss_fine", vm["loss_coarse"])
-            psnr = -10.0 * math.log10(last) if last > 0 else float("inf")
-            lr = optimizer.param_groups[0]["lr"]
-            if logger is not None:
-                logger.log_training(TrainingMetrics(iteration=iteration, loss=vm["loss"], loss_coarse=vm["loss_coarse"],
-                                                    loss_fine=vm.get("loss_fine"), psnr=psnr, learning_rate=lr,
-                                                    time_per_iter=batch_time, rays_per_sec=B / batch_time))
-                if iteration % config.train.log_every == 0:
-                    log(f"[{iteration:7d}/{config.train.num_iterations}] loss: {vm['loss']:.5f} | psnr: {psnr:.2f} | "
-                        f"lr: {lr:.2e} | rays/s: {B / batch_time:.0f} | time: {(time.time() - start) / 60:.1f}min")
-                if iteration % config.train.val_every == 0 and iteration > 0:
+            now = time.time()
+            log_iteration(lagged.push(mean_over_ranks([m[k] for k in keys], process_group),
+                                      (iteration, keys, optimizer.param_groups[0]["lr"], now - t_prev)))
+            t_prev = now
+            if logger is not None and iteration > 0 and (iteration % config.train.val_every == 0
+                                                         or iteration % config.train.save_every == 0):
+                log_iteration(lagged.flush())
+                if iteration % config.train.val_every == 0:
                     vmx = evaluate(renderer, val_data, logger, iteration, num_images=5, lpips_metric=lpips_metric)
                     logger.log_validation(vmx)
                     is_best = vmx.psnr > best_psnr
@@ -288,9 +310,11 @@ def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
                         + (" (best)" if is_best else ""))
                     save_checkpoint(output_dir, iteration, model_coarse, model_fine, optimizer, config, noise_config,
                                     metrics={"psnr": vmx.psnr, "ssim": vmx.ssim}, is_best=is_best)
-                elif iteration % config.train.save_every == 0 and iteration > 0:
+                else:
                     save_checkpoint(output_dir, iteration, model_coarse, model_fine, optimizer, config, noise_config)
+                t_prev = time.time()  # the next iteration's time excludes the validation
             iteration += 1
+    log_iteration(lagged.flush())
     result = {"model_coarse": model_coarse, "model_fine": model_fine, "output_dir": output_dir,
               "best_psnr": best_psnr}
     if logger is not None:
@@ -309,7 +333,7 @@ def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
 
 
 def build_arg_parser():
-    """Reference train.py:580-657 flags (same names and defaults) plus ``--precision``."""
+    """Reference train.py:580-657 flags (same names and defaults) plus ``--precision`` and ``--graph``."""
     import argparse
     ap = argparse.ArgumentParser(description="Train NeRF with optional pose noise (MI355X HIP path)")
     ap.add_argument("--scene", type=str, default="lego")
@@ -334,6 +358,8 @@ def build_arg_parser():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16", "fp16"],
                     help="MLP operand precision (fp32 = the reference's numerics)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the training step from a hipGraph (one process; same results as eager)")
     return ap
 
 
@@ -362,7 +388,7 @@ def main(argv=None) -> None:
         name = [generate_experiment_name(a.scene, noise_config)]
         dist.broadcast_object_list(name, src=0, group=pg)
         cfg.train.experiment_name = name[0]
-    train(cfg, noise_config, process_group=pg)
+    train(cfg, noise_config, process_group=pg, graph=a.graph)
     if pg is not None:
         import torch.distributed as dist
         dist.destroy_process_group()

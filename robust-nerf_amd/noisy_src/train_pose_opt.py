@@ -40,7 +40,7 @@ from .config import RenderConfig
 from .config import NeRFConfig
 from .data import BlenderData, load_blender_data
 from .data_pose_opt import PixelBatch, PixelSampler, create_pixel_dataset
-from .engine import PoseTrainer, check_run_args, init_distributed, mean_over_ranks, rank_slice
+from .engine import LaggedScalars, PoseTrainer, check_run_args, init_distributed, mean_over_ranks, rank_slice
 from .logger import ExperimentLogger, TrainingMetrics, ValidationMetrics
 from .metrics import LPIPSMetric, compute_mse, compute_psnr, compute_ssim
 from .model import NeRF
@@ -341,30 +341,41 @@ def train_with_pose_optimization(config: NeRFConfig, noise_config: Optional[Nois
     val_idx = torch.arange(val_data.images.shape[0], device=device)
     start = time.time()
     best_psnr = 0.0
+    lagged = LaggedScalars()  # logged losses read one iteration late: no per-step host sync
+    t_prev = time.time()
+
+    def log_iteration(done):
+        if done is None or logger is None:
+            return
+        vals, (it, keys, lr, now, batch_time) = done
+        vm = dict(zip(keys, vals))
+        last = vm.get("loss_fine", vm["loss_coarse"])
+        psnr = -10.0 * math.log10(last) if last > 0 else float("inf")
+        logger.log_training(TrainingMetrics(iteration=it, loss=vm["loss"], loss_coarse=vm["loss_coarse"],
+                                            loss_fine=vm.get("loss_fine"), psnr=psnr, learning_rate=lr,
+                                            time_per_iter=batch_time, rays_per_sec=B / batch_time))
+        if it % config.train.log_every == 0:
+            log(f"[{it:7d}/{config.train.num_iterations}] loss: {vm['loss']:.5f} | psnr: {psnr:.2f} | "
+                f"lr: {lr:.2e} | poses: {'optimizing' if now else 'frozen'} | "
+                f"time: {(time.time() - start) / 60:.1f}min")
+
     for iteration in range(config.train.num_iterations):
         batch = pixel_sampler.sample_batch()  # the global batch, identical on every rank
         now = iteration >= pose_opt_delay
         t_rand = torch.rand(B, rc.num_samples, device=device) if rc.perturb else None
         u = torch.rand(B, rc.num_samples_fine, device=device) if (rc.use_hierarchical and model_fine) else None
         sl = rank_slice(B, rank, world) if world > 1 else slice(0, B)
-        t0 = time.time()
         m = trainer.step(batch.slice(sl) if world > 1 else batch, optimize_poses=now,
                          t_rand=None if t_rand is None else t_rand[sl], u=None if u is None else u[sl])
         keys = ["loss", "loss_coarse"] + (["loss_fine"] if "loss_fine" in m else [])
-        vm = dict(zip(keys, mean_over_ranks([m[k] for k in keys], process_group).tolist()))
-        batch_time = time.time() - t0
-        last = vm.get("loss_fine", vm["loss_coarse"])
-        psnr = -10.0 * math.log10(last) if last > 0 else float("inf")
-        lr = optimizer_nerf.param_groups[0]["lr"]
+        t_now = time.time()
+        log_iteration(lagged.push(mean_over_ranks([m[k] for k in keys], process_group),
+                                  (iteration, keys, optimizer_nerf.param_groups[0]["lr"], now, t_now - t_prev)))
+        t_prev = t_now
         if logger is None:
             continue
-        logger.log_training(TrainingMetrics(iteration=iteration, loss=vm["loss"], loss_coarse=vm["loss_coarse"],
-                                            loss_fine=vm.get("loss_fine"), psnr=psnr, learning_rate=lr,
-                                            time_per_iter=batch_time, rays_per_sec=B / batch_time))
-        if iteration % config.train.log_every == 0:
-            log(f"[{iteration:7d}/{config.train.num_iterations}] loss: {vm['loss']:.5f} | psnr: {psnr:.2f} | "
-                f"lr: {lr:.2e} | poses: {'optimizing' if now else 'frozen'} | "
-                f"time: {(time.time() - start) / 60:.1f}min")
+        if iteration > 0 and (iteration % config.train.val_every == 0 or iteration % config.train.save_every == 0):
+            log_iteration(lagged.flush())
         if iteration % config.train.val_every == 0 and iteration > 0:
             pe = camera_params.compute_pose_errors(gt_train_poses)
             vmx = evaluate_with_poses(model_coarse, model_fine, camera_params, val_data, val_idx, rc, logger,
@@ -378,10 +389,13 @@ def train_with_pose_optimization(config: NeRFConfig, noise_config: Optional[Nois
                                        optimizer_nerf, optimizer_poses, config, noise_config,
                                        metrics={"psnr": vmx.psnr, "ssim": vmx.ssim}, pose_errors=pe,
                                        is_best=is_best)
+            t_prev = time.time()  # the next iteration's time excludes the validation
         elif iteration % config.train.save_every == 0 and iteration > 0:
             pe = camera_params.compute_pose_errors(gt_train_poses)
             save_checkpoint_with_poses(output_dir, iteration, model_coarse, model_fine, camera_params,
                                        optimizer_nerf, optimizer_poses, config, noise_config, pose_errors=pe)
+            t_prev = time.time()
+    log_iteration(lagged.flush())
     result = {"model_coarse": model_coarse, "model_fine": model_fine, "camera_params": camera_params,
               "output_dir": output_dir, "pose_errors": camera_params.compute_pose_errors(gt_train_poses)}
     if logger is not None:

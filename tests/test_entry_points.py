@@ -98,6 +98,28 @@ def test_train_cli_coarse_only(tmp_path):
     assert head == "iteration,loss,loss_coarse,psnr,learning_rate,time_per_iter,rays_per_sec"
 
 
+def test_train_cli_graph_matches_eager(tmp_path):
+    """``--graph``: iteration 0 eager, then the step replayed from a hipGraph; an epoch's
+    short final batch (768 rays / 100) runs eagerly between replays, and validation runs
+    mid-way.  The weights and every logged loss equal the eager run's bit for bit."""
+    from noisy_src.train import main
+    _scene(tmp_path / "data")
+    cks, rows = {}, {}
+    for name, extra in (("e", []), ("g", ["--graph"])):
+        main(["--data_root", str(tmp_path / "data"), "--img_scale", "1.0", "--batch_size", "100", "--num_iters", "10",
+              "--val_every", "4", "--save_every", "100", "--output_dir", str(tmp_path / "out"), "--exp_name", name,
+              "--precision", "bf16"] + extra)
+        run = tmp_path / "out" / name
+        cks[name] = torch.load(run / "checkpoint_latest.pt", weights_only=True, map_location="cpu")
+        rows[name] = [r.split(",")[:3] for r in (run / "logs" / "train_metrics.csv").read_text().splitlines()]
+    assert len(rows["g"]) == 11 and rows["g"] == rows["e"]
+    for net in ("model_coarse", "model_fine"):
+        for k, v in cks["e"][net].items():
+            assert torch.equal(v, cks["g"][net][k]), (net, k)
+    for k, v in cks["e"]["optimizer"]["state"].items():
+        assert torch.equal(v["exp_avg"], cks["g"]["optimizer"]["state"][k]["exp_avg"]), k
+
+
 def test_train_pose_opt_cli(tmp_path):
     from noisy_src.train_pose_opt import main
     _scene(tmp_path / "data")
