@@ -181,11 +181,11 @@ class Trainer:
         gs = self.reducer.prescale if self.reducer is not None else 1.0  # DP: 1/world in the seed
         loss_c = ops.mse_loss(out["rgb_coarse"], target_rgb, gs)
         loss = loss_c
-        metrics = {"loss_coarse": loss_c}
+        metrics = {"loss_coarse": loss_c.detach()}  # metrics hold no autograd graph
         if "rgb_fine" in out:
             loss_f = ops.mse_loss(out["rgb_fine"], target_rgb, gs)
             loss = loss_c + loss_f
-            metrics["loss_fine"] = loss_f
+            metrics["loss_fine"] = loss_f.detach()
         loss.backward(ops.unit_grad(loss.device))
         if self.reducer is not None:
             flats = [flat for _, flat in self.reducer.pending]
@@ -365,11 +365,11 @@ class PoseTrainer:
         gs = self.reducer.prescale if self.reducer is not None else 1.0  # DP: 1/world in the seed
         loss_c = ops.mse_loss(out["rgb_coarse"], target, gs)
         loss = loss_c
-        metrics = {"loss_coarse": loss_c}
+        metrics = {"loss_coarse": loss_c.detach()}  # metrics hold no autograd graph
         if "rgb_fine" in out:
             loss_f = ops.mse_loss(out["rgb_fine"], target, gs)
             loss = loss_c + loss_f
-            metrics["loss_fine"] = loss_f
+            metrics["loss_fine"] = loss_f.detach()
         bwd = loss
         if optimize_poses:
             # the regulariser is replicated on every rank: its gradient carries the seed's
