@@ -101,11 +101,7 @@ def rocprof_summary(prec: str):
 
 
 def _flops_of(entry: str, M: int) -> float:
-    if entry == "nr_mlp_forward":
-        return 2.0 * MACS_PER_EVAL * M
-    if entry == "nr_mlp_backward_dx":
-        return 2.0 * MACS_DX * M
-    return 0.0
+    return 2.0 * mfma_macs_of(entry) * M
 
 
 def _alg_bytes_of(entry: str, M: int, prec: str, n_params: int) -> float:
@@ -128,10 +124,25 @@ def bound_of(entry: str, M: int, prec: str, counted_bytes):
     return ("hbm" if t_hbm >= t_mfma else "mfma"), t_mfma * 1e3, t_hbm * 1e3
 
 
+def mfma_macs_of(entry: str) -> int:
+    """MFMA multiply-adds per sample of one fused-MLP launch (SURVEY.md §8d basis): the
+    forward's layers, the dX chain's W^T products, dW's outer products (one per weight)."""
+    return {"nr_mlp_forward": MACS_PER_EVAL, "nr_mlp_backward_dx": MACS_DX, "nr_mlp_backward_dw": MACS_PER_EVAL,
+            "nr_mlp_backward_dxdw": MACS_DX + MACS_PER_EVAL}.get(entry, 0)
+
+
+def mfma_roofline(entry: str, M: int, ms: float, prec: str):
+    """the MLP is bounded by its MFMA FLOPs.  (achieved TFLOP/s, frac of
+    the dense peak, work description) of one launch."""
+    macs = mfma_macs_of(entry)
+    tf = 2.0 * macs * M / (ms * 1e-3) / 1e12
+    return tf, tf / PEAK_TFLOPS[prec], f"2 x {macs} MAC x {M} samples"
+
+
 def roofline_of(entry: str, M: int, ms: float, prec: str, n_params: int, counted_bytes=None):
-    """(bound, achieved, peak, unit, work-per-launch description) of one fused-MLP launch.
-    ``achieved`` is ALGORITHMIC work (FLOPs, or the bytes the kernel must move) per
-    launch over the launch time, against the peak of the bound that ``bound_of`` picks."""
+    """(bound, achieved, peak, unit, work-per-launch description) of one fused-MLP launch
+    on the stored-activation HBM basis: the bytes THIS design stores / reads (a design
+    choice, not the algorithm's: the headline roofline is ``mfma_roofline``)."""
     esize = 4 if prec == "fp32" else 2
     bound, _, _ = bound_of(entry, M, prec, counted_bytes)
     if entry in ("nr_mlp_forward", "nr_mlp_backward_dx") and bound == "mfma":
@@ -420,7 +431,10 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true",
-                    help="replay the training step as one captured hipGraph (engine.GraphedTrainer; N=1)")
+                    help="replay the training step as one captured hipGraph (engine.GraphedTrainer; with "
+                         "data parallelism the RCCL all-reduces are captured too)")
+    ap.add_argument("--dp", action="store_true",
+                    help="join an RCCL process group even at N=1 (the data-parallel step, all-reduce hooks active)")
     ap.add_argument("--pose-opt", action="store_true",
                     help="BASELINE cfg #3: joint pose optimisation step (train_pose_opt, poses optimising)")
     args = ap.parse_args()
@@ -440,8 +454,16 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
-    if world > 1:
+    if world > 1 or args.dp:
         import torch.distributed as dist
+        if world == 1:  # --dp without torchrun: a world-1 group of this process
+            import socket
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", str(port)), ("RANK", "0"),
+                         ("WORLD_SIZE", "1")):
+                os.environ.setdefault(k, v)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -519,8 +541,10 @@ def main():
         # one captured hipGraph per step: no Python runs inside the timed region, so the
         # dominant kernel is timed over the eager warm-up steps above (and by rocprof)
         from noisy_src.engine import GraphedTrainer
-        if world > 1 or args.pose_opt:
-            raise SystemExit("--graph: single-GPU Trainer steps only")
+        if args.pose_opt:
+            raise SystemExit("--graph: Trainer steps only (not --pose-opt)")
+        if pg is not None and backend != "nccl":
+            raise SystemExit("--graph with data parallelism needs the nccl (RCCL) backend")
         gtr = GraphedTrainer(trainer, *pool[0], warmup=2)
 
         def step(k):  # noqa: F811
@@ -564,6 +588,7 @@ def main():
     dom_traffic = traffic_of(kern, M, args.precision)
     n_params = mf.flat_params().numel()
     bound, achieved, peak, unit, work = roofline_of(entry, M, ms, args.precision, n_params, dom_traffic)
+    mf_tf, _, mf_work = mfma_roofline(entry, M, ms, args.precision)
     # the committed rocprofv3 kernel trace of this tree (same bench command): its average
     # for the dominant kernel, and the fraction it gives (the live one is `frac`)
     rp_rows, rp_src = rocprof_summary(args.precision)
@@ -593,30 +618,40 @@ def main():
             "global_batch": world * B,
             "num_samples": rcfg.num_samples,
             "num_samples_fine": rcfg.num_samples_fine,
-            "parallelism": f"dp{world}",
+            "parallelism": f"dp{world}" + (" (RCCL process group, all-reduce in the step)" if pg is not None
+                                           and world == 1 else ""),
             **({"execution": "hipGraph replay (engine.GraphedTrainer)"} if args.graph else {}),
         },
+        # headline: the dominant kernel on SURVEY §8d's MFMA basis (algorithmic FLOPs per
+        # launch over its launch time); the stored-activation HBM view rides beside it
         "roofline": {
-            "bound": bound,
+            "bound": "mfma",
             "kernel": f"{kern[0]} via {entry} (M={M} samples, fine net)",
-            "achieved": round(achieved * ms / rp_ms if rp_ms else achieved, 2),
-            "peak": peak,
-            "unit": unit,
+            "achieved": round(mf_tf * ms / rp_ms if rp_ms else mf_tf, 2),
+            "peak": PEAK_TFLOPS[args.precision],
+            "unit": "TFLOP/s",
             # frac: from the committed rocprof kernel-trace average of these sources when
             # one exists (reproducible from profiles/), else from the live launch time
-            "frac": round((achieved * ms / rp_ms if rp_ms else achieved) / peak, 4),
+            "frac": round((mf_tf * ms / rp_ms if rp_ms else mf_tf) / PEAK_TFLOPS[args.precision], 4),
+            "frac_mfma": round((mf_tf * ms / rp_ms if rp_ms else mf_tf) / PEAK_TFLOPS[args.precision], 4),
             "frac_basis": (f"rocprof_ms: timed-region average of {rp_src} (same source_hash)" if rp_ms
                            else "launch_ms: HIP events on the launching stream over the eager warm-up steps "
                            "(a graph replay runs no Python)" if args.graph
                            else "launch_ms: live HIP events on the launching stream over the timed region"),
             "traffic": dom_traffic,
-            "work_per_launch": work,
+            "work_per_launch": mf_work,
             "launch_ms": round(ms, 4),
             "launches": n_launch,
-            "frac_live": round(achieved / peak, 4),
+            "frac_live": round(mf_tf / PEAK_TFLOPS[args.precision], 4),
             "rocprof_ms": round(rp_ms, 4) if rp_ms else None,
             "rocprof_source": rp_src if rp_ms else None,
             "source_hash": source_hash(),
+            "stored_activation_bytes_design": {
+                "bound": bound, "achieved": round(achieved * ms / rp_ms if rp_ms else achieved, 2), "peak": peak,
+                "unit": unit, "frac": round((achieved * ms / rp_ms if rp_ms else achieved) / peak, 4),
+                "work_per_launch": work,
+                "note": "bytes this decomposition chooses to store and re-read (saved activations, dz), "
+                        "not algorithmic work"},
         },
         # per fused-MLP launch: live ms (last warm-up steps), counted PMC bytes and their
         # rate, MFMA / HBM floors and the bound they give (profiles/traffic.json)

@@ -233,6 +233,24 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved,
 int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M,
                            const void* workspace, float* g_params,
                            nr_stream_t stream);
+/* dx + dw as ONE layer-pipelined launch (16-bit): one workgroup per layer and
+ * sample range, dz handed between layers through on-chip-resident rings in the
+ * workspace instead of HBM images; writes the same per-chunk slabs (bit-identical
+ * to dx then dw), so nr_mlp_backward_reduce follows it.  g_x / g_d as
+ * nr_mlp_backward_dx.  Outside its envelope (fp32, more than one skip layer,
+ * fewer CUs than pipelines x stages) it runs dx then dw itself.              */
+int nr_mlp_backward_dxdw(const NrMlpConfig* cfg, const void* packed,
+                         const float* params, const float* x, const float* d,
+                         int64_t M, const float* rgb, const float* sigma,
+                         const void* saved, const float* g_rgb,
+                         const float* g_sigma, float* g_x, float* g_d,
+                         void* workspace, nr_stream_t stream);
+/* 1 if nr_mlp_backward_dxdw runs the pipelined kernel for (cfg, M) on the
+ * current device, else 0.                                                   */
+int nr_mlp_backward_pipelined(const NrMlpConfig* cfg, int64_t M);
+/* Byte offset in the workspace of the pipelined backward's status word (0 = ok,
+ * nonzero = a bounded wait timed out and the gradients are invalid), or -1. */
+int64_t nr_mlp_pipe_status_offset(const NrMlpConfig* cfg, int64_t M);
 
 /* ---- A13: optimizer tail  (noisy_src/train.py:112-117, train_pose_opt.py:398-409)
  * Sum of squares of n fp32 values added into *acc (device scalar, caller-zeroed):

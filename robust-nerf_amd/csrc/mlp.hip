@@ -2283,6 +2283,8 @@ __global__ void __launch_bounds__(kSumsqThreads) adam_multi_kernel(AdamMultiArgs
     }
 }
 
+#include "mlp_pipe.inc"
+
 }  // namespace nr
 
 using namespace nr;
@@ -2452,6 +2454,173 @@ int launch_dinput(const MlpPlan& p, const DinArgs& a, hipStream_t s) {
 #undef NR_DIN
     set_error("nr_mlp_backward_dx: no input-gradient kernel for XB=%d DB=%d", p.XB, p.DB);
     return NR_EARG;
+}
+
+// 16-bit g_x / g_d: one MFMA pass over the stored dz images of the x_enc-reading
+// layers and of dz_c (mlp_dinput_kernel), after either backward form wrote them
+int input_grads16(const MlpPlan& p, const MlpSizes& z, const char* packed, const float* x, const float* d, float* g_x,
+                  float* g_d, const char* ws, int64_t M, hipStream_t s) {
+    const int n = p.n_layers;
+    DinArgs da;
+    std::memset(&da, 0, sizeof(da));
+    da.packed = packed;
+    da.ws = ws;
+    da.x = x;
+    da.d = d;
+    da.g_x = g_x;
+    da.g_d = g_d;
+    da.M = M;
+    da.tiles = z.tiles;
+    da.L = p.L;
+    da.Ld = p.Ld;
+    da.inv_gscale = 1.0f / grad_scale(p.prec);
+    // layer 0 reads x_enc alone; a skip layer's W^T chunk is [h (8) | x_enc (XB)]
+    for (int l = 0; l < n; ++l) {
+        if (l > 0 && !is_skip(p, l - 1)) continue;
+        da.a_off[da.nsrc] = p.lin[l].pk_bwd;
+        da.a_kb[da.nsrc] = p.lin[l].KB;
+        da.a_p0[da.nsrc] = p.lin[l].KB - p.XB;
+        da.dz_off[da.nsrc] = z.ws_off[WS_DZ0 + l];
+        da.nsrc++;
+    }
+    // dir's W^T chunk is [feat (8) | d_enc (DB)], one chunk per dz_c block
+    da.dir_a_off = p.lin[n + 1].pk_bwd;
+    da.dir_kb = p.lin[n + 1].KB;
+    da.dir_p0 = kHB;
+    da.nc = p.lin[n + 1].NB;
+    da.dz_dir_off = z.ws_off[p.ws_dir];
+    return p.prec == NR_PREC_BF16 ? launch_dinput<NR_PREC_BF16>(p, da, s) : launch_dinput<NR_PREC_FP16>(p, da, s);
+}
+
+// ---- fused layer-pipelined backward (mlp_pipe.inc) ----
+// The stage layout of a plan, or false when the plan is not one the pipeline covers:
+// 16-bit, exactly one x-job (layer 0 and at most one skip layer) and the split plan's
+// job order (x, h-jobs 1..n-1, feat, dir), whose slabs the stages write.
+bool pipe_layout(const MlpPlan& p, const MlpSizes& z, PipeArgs& a, int& NX) {
+    if (p.fpb != 2 || z.pipe_edges != p.n_layers + 1) return false;
+    const int n = p.n_layers;
+    if (p.n_jobs != n + 2 || n + 2 > kPipeMaxStages) return false;
+    const DwJob& xj = p.job[0];
+    NX = xj.ndz;
+    if (NX < 1 || NX > 2 || xj.nin != 1 || xj.in[0].is_ws || xj.in[0].tensor != SV_XENC) return false;
+    int xl[2] = {-1, -1};
+    for (int x = 0; x < NX; ++x) {
+        if (!xj.dz[x].is_ws) return false;
+        xl[x] = xj.dz[x].tensor - WS_DZ0;
+    }
+    if (xl[0] != 0 || (NX == 2 && (xl[1] < 1 || xl[1] >= n))) return false;
+    for (int i = 1; i < n; ++i) {
+        const DwJob& j = p.job[i];
+        if (j.ndz != 1 || j.nin != 1 || !j.dz[0].is_ws || j.dz[0].tensor != WS_DZ0 + i || j.in[0].is_ws ||
+            j.in[0].tensor != SV_H0 + i - 1)
+            return false;
+    }
+    const int jfeat = n, jdir = n + 1;
+    if (p.job[jfeat].dz[0].tensor != p.ws_feat || p.job[jdir].dz[0].tensor != p.ws_dir || p.job[jfeat].NBz != kHB + 1)
+        return false;
+    auto x_of = [&](int layer) { return layer == xl[0] ? 0 : (NX == 2 && layer == xl[1] ? 1 : -1); };
+    // edge j carries dz_j (j < n) or dz_feat (j = n); an x-layer j >= 1 has S_X as its second consumer
+    auto ncons = [&](int j) { return (j >= 1 && x_of(j) >= 0) ? 2 : 1; };
+    a.nstage = n + 2;
+    a.nedge = n + 1;
+    for (int s = 0; s < a.nstage; ++s) {
+        PipeStageDesc& st = a.st[s];
+        std::memset(&st, 0, sizeof(st));
+        st.in_edge = st.out_edge = -1;
+        if (s == 0) {
+            st.kind = PK_DIR;
+            st.out_edge = n;
+            st.out_ncons = 1;
+            st.job = jdir;
+            st.job2 = jfeat;
+            st.mask_layer = n;
+            st.w_img = p.lin[n + 1].pk_bwdr;
+            st.ws_store[0] = z.ws_off[p.ws_dir];
+        } else if (s == 1) {
+            st.kind = PK_FEAT;
+            st.in_edge = n;
+            st.out_edge = n - 1;
+            st.out_ncons = ncons(n - 1);
+            st.job = jfeat;
+            st.mask_layer = n - 1;
+            st.w_img = p.lin[n].pk_bwdr;
+            st.sv_in = z.saved_off[SV_H0 + n - 1];
+        } else if (s <= n) {
+            const int i = n + 1 - s;
+            st.kind = PK_TRUNK;
+            st.in_edge = i;
+            st.out_edge = i - 1;
+            st.out_ncons = ncons(i - 1);
+            st.job = i;
+            st.mask_layer = i - 1;
+            st.w_img = p.lin[i].pk_bwdr;
+            st.sv_in = z.saved_off[SV_H0 + i - 1];
+        } else {
+            st.kind = PK_X;
+            for (int x = 0; x < NX; ++x) {
+                st.x_edge[x] = xl[x];
+                st.x_cons[x] = xl[x] >= 1 ? 1 : 0;
+                st.ws_store[x] = z.ws_off[WS_DZ0 + xl[x]];
+            }
+            st.job = 0;
+            st.sv_in = z.saved_off[SV_XENC];
+        }
+    }
+    for (int j = 0; j < p.n_jobs; ++j) {
+        a.job_slab[j] = p.job[j].slab_off;
+        a.job_ld[j] = p.job[j].KB * 32 + 1;
+    }
+    return true;
+}
+
+// CUs of the current device (the pipeline needs every workgroup resident at once)
+int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (cus[dev] == 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+        cus[dev] = v;
+    }
+    return cus[dev];
+}
+
+template <int PREC, int XB, int DB, int NX>
+bool pipe_resident_one_per_cu() {
+    static int ok = -1;  // one query per instantiation
+    if (ok < 0) {
+        int nb = 0;
+        const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &nb, reinterpret_cast<const void*>(&mlp_bwd_pipe_kernel<PREC, XB, DB, NX>), kPipeThreads,
+            pipe_lds_bytes(XB, DB, NX));
+        ok = (e == hipSuccess && nb >= 1) ? 1 : 0;
+    }
+    return ok == 1;
+}
+
+template <int PREC>
+int launch_pipe(const MlpPlan& p, const PipeArgs& a, int NX, hipStream_t s, bool* launched) {
+    *launched = false;
+    const dim3 grid(static_cast<unsigned>(a.npipe * a.nstage)), block(kPipeThreads);
+#define NR_PIPE(XB_, DB_, NX_)                                                                               \
+    if (p.XB == XB_ && p.DB == DB_ && NX == NX_) {                                                           \
+        if (!pipe_resident_one_per_cu<PREC, XB_, DB_, NX_>()) return NR_OK;                                  \
+        hipLaunchKernelGGL((mlp_bwd_pipe_kernel<PREC, XB_, DB_, NX_>), grid, block, pipe_lds_bytes(XB_, DB_, NX_), \
+                           s, a);                                                                            \
+        *launched = true;                                                                                    \
+        return check_launch("nr_mlp_backward_dxdw");                                                         \
+    }
+    NR_PIPE(2, 1, 2)
+#ifndef NR_MLP_DEV
+    // the reference's encodings (pos_freqs 10: XB 2), with / without view dirs and skip;
+    // other encodings run the split backward
+    NR_PIPE(2, 1, 1)
+    NR_PIPE(2, 0, 2)
+    NR_PIPE(2, 0, 1)
+#endif
+#undef NR_PIPE
+    return NR_OK;  // no instance: the caller runs the split backward
 }
 
 }  // namespace
@@ -2820,35 +2989,7 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     if (split_in) {
         const int rc = chain16();
         if (rc != NR_OK) return rc;
-        DinArgs da;
-        std::memset(&da, 0, sizeof(da));
-        da.packed = b.packed;
-        da.ws = b.ws;
-        da.x = x;
-        da.d = d;
-        da.g_x = g_x;
-        da.g_d = g_d;
-        da.M = M;
-        da.tiles = z.tiles;
-        da.L = p.L;
-        da.Ld = p.Ld;
-        da.inv_gscale = b.inv_gscale;
-        // layer 0 reads x_enc alone; a skip layer's W^T chunk is [h (8) | x_enc (XB)]
-        for (int l = 0; l < n; ++l) {
-            if (l > 0 && !is_skip(p, l - 1)) continue;
-            da.a_off[da.nsrc] = p.lin[l].pk_bwd;
-            da.a_kb[da.nsrc] = p.lin[l].KB;
-            da.a_p0[da.nsrc] = p.lin[l].KB - p.XB;
-            da.dz_off[da.nsrc] = z.ws_off[WS_DZ0 + l];
-            da.nsrc++;
-        }
-        // dir's W^T chunk is [feat (8) | d_enc (DB)], one chunk per dz_c block
-        da.dir_a_off = p.lin[n + 1].pk_bwd;
-        da.dir_kb = p.lin[n + 1].KB;
-        da.dir_p0 = kHB;
-        da.nc = p.lin[n + 1].NB;
-        da.dz_dir_off = z.ws_off[p.ws_dir];
-        return p.prec == NR_PREC_BF16 ? launch_dinput<NR_PREC_BF16>(p, da, s) : launch_dinput<NR_PREC_FP16>(p, da, s);
+        return input_grads16(p, z, b.packed, x, d, g_x, g_d, b.ws, M, s);
     }
     if (p.prec != NR_PREC_FP32 && !wx) return chain16();
     if (p.prec == NR_PREC_BF16) return launch_bwd<NR_PREC_BF16, true>(p, b, s);
@@ -2966,15 +3107,103 @@ int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M, const void* worksp
     return NR_OK;
 }
 
+int nr_mlp_backward_dxdw(const NrMlpConfig* cfg, const void* packed, const float* params, const float* x,
+                         const float* d, int64_t M, const float* rgb, const float* sigma, const void* saved,
+                         const float* g_rgb, const float* g_sigma, float* g_x, float* g_d, void* workspace,
+                         nr_stream_t stream) {
+    MlpPlan p;
+    if (!plan_or_error(cfg, &p)) return NR_EARG;
+    NR_REQUIRE(packed && params && x && rgb && sigma && saved && g_rgb && g_sigma && workspace && M >= 0,
+               "nr_mlp_backward_dxdw: null pointer");
+    NR_REQUIRE(!g_d || (d && p.use_vd), "nr_mlp_backward_dxdw: g_d needs d and use_view_dirs");
+    NR_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0 && (reinterpret_cast<uintptr_t>(saved) & 15) == 0,
+               "nr_mlp_backward_dxdw: saved and workspace must be 16-byte aligned");
+    if (M == 0) return NR_OK;
+    NR_REQUIRE(M <= (int64_t{1} << 36), "nr_mlp_backward_dxdw: M beyond 2^36 samples");
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const MlpSizes z = make_sizes(p, M);
+    PipeArgs a;  // ~3 KB of kernel arguments, copied by the launch
+    std::memset(&a, 0, sizeof(a));
+    int NX = 0;
+    const bool layout = pipe_layout(p, z, a, NX);
+    a.npipe = z.chunks;
+    const int cus = device_cus();
+    bool launched = false;
+    if (layout && cus > 0 && a.npipe * a.nstage <= cus) {
+        char* ws = static_cast<char*>(workspace);
+        a.packed = static_cast<const char*>(packed);
+        a.saved = static_cast<const char*>(saved);
+        a.ws = ws;
+        a.rgb = rgb;
+        a.sigma = sigma;
+        a.g_rgb = g_rgb;
+        a.g_sigma = g_sigma;
+        a.gscale = grad_scale(p.prec);
+        a.pose = (g_x || g_d) ? 1 : 0;
+        a.M = M;
+        a.tiles = z.tiles;
+        a.tpp = static_cast<int>(ceil_div_ll(z.tiles, z.chunks));  // = the split dW's tiles_per_chunk
+        a.slabs = reinterpret_cast<float*>(ws + z.slab_off);
+        a.slab_floats_per_chunk = p.slab_floats_per_chunk;
+        a.ring = ws + z.pipe_ring_off;
+        a.ring_pipe_bytes = z.pipe_ring_pipe_bytes;
+        a.status = reinterpret_cast<unsigned*>(ws + z.pipe_flags_off);
+        a.flags = a.status + kPipeStatusWordsHead;
+        a.mask_off = z.mask_off;
+        a.n_mask = p.n_mask;
+        a.sv_feat = z.saved_off[p.sv_feat];
+        a.sv_denc = z.saved_off[p.sv_denc];
+        a.sv_hc = z.saved_off[p.sv_hc];
+        a.sv_hlast = z.saved_off[SV_H0 + p.n_layers - 1];
+        a.vrgb = p.vrgb;
+        a.vhead = p.vhead;
+        // every flag / status word starts at 0 in every call (a memset node under capture)
+        const hipError_t e = hipMemsetAsync(ws + z.pipe_flags_off, 0, static_cast<size_t>(z.pipe_flags_bytes), s);
+        if (e != hipSuccess) {
+            set_error("nr_mlp_backward_dxdw: %s", hipGetErrorString(e));
+            return static_cast<int>(e);
+        }
+        const int rc = p.prec == NR_PREC_BF16 ? launch_pipe<NR_PREC_BF16>(p, a, NX, s, &launched)
+                                              : launch_pipe<NR_PREC_FP16>(p, a, NX, s, &launched);
+        if (rc) return rc;
+    }
+    if (!launched) {
+        // outside the pipeline's envelope (fp32, several skips, too few CUs): the split backward
+        const int rc = nr_mlp_backward_dx(cfg, packed, params, x, d, M, rgb, sigma, saved, g_rgb, g_sigma, g_x, g_d,
+                                          workspace, stream);
+        if (rc) return rc;
+        return nr_mlp_backward_dw(cfg, M, saved, workspace, stream);
+    }
+    if (g_x || g_d) return input_grads16(p, z, static_cast<const char*>(packed), x, d, g_x, g_d,
+                                         static_cast<const char*>(workspace), M, s);
+    return NR_OK;
+}
+
+int nr_mlp_backward_pipelined(const NrMlpConfig* cfg, int64_t M) {
+    MlpPlan p;
+    if (!plan_or_error(cfg, &p) || M <= 0) return 0;
+    const MlpSizes z = make_sizes(p, M);
+    PipeArgs a;
+    int NX = 0;
+    if (!pipe_layout(p, z, a, NX)) return 0;
+    const int cus = device_cus();
+    return cus > 0 && z.chunks * (p.n_layers + 2) <= cus ? 1 : 0;
+}
+
+int64_t nr_mlp_pipe_status_offset(const NrMlpConfig* cfg, int64_t M) {
+    MlpPlan p;
+    if (!plan_or_error(cfg, &p) || M <= 0) return -1;
+    const MlpSizes z = make_sizes(p, M);
+    return p.fpb == 2 ? z.pipe_flags_off : -1;
+}
+
 int nr_mlp_backward(const NrMlpConfig* cfg, const void* packed, const float* params, const float* x, const float* d,
                     int64_t M, const float* rgb, const float* sigma, const void* saved, const float* g_rgb,
                     const float* g_sigma, float* g_params, float* g_x, float* g_d, void* workspace,
                     nr_stream_t stream) {
     NR_REQUIRE(g_params, "nr_mlp_backward: null g_params");
-    int rc = nr_mlp_backward_dx(cfg, packed, params, x, d, M, rgb, sigma, saved, g_rgb, g_sigma, g_x, g_d, workspace,
-                                stream);
-    if (rc) return rc;
-    rc = nr_mlp_backward_dw(cfg, M, saved, workspace, stream);
+    int rc = nr_mlp_backward_dxdw(cfg, packed, params, x, d, M, rgb, sigma, saved, g_rgb, g_sigma, g_x, g_d,
+                                  workspace, stream);
     if (rc) return rc;
     return nr_mlp_backward_reduce(cfg, M, workspace, g_params, stream);
 }

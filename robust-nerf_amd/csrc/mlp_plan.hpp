@@ -141,10 +141,20 @@ struct MlpSizes {
     int64_t mask_off;                  // bytes
     int64_t saved_bytes;
     int64_t ws_off[kMaxTrunk + 3];     // bytes
-    int chunks;                        // dW split over sample tiles
+    int chunks;                        // dW split over sample tiles (= pipelines of the fused backward)
     int64_t slab_off;                  // bytes
+    // fused 16-bit backward (mlp_pipe.inc): status + flag words (zeroed every call), then
+    // the dz rings, [pipeline][edge][slot] 16-KB tiles; edges = dz_0 .. dz_{n-1}, dz_feat
+    int pipe_edges;
+    int64_t pipe_flags_off, pipe_flags_bytes;  // bytes
+    int64_t pipe_ring_off, pipe_ring_pipe_bytes;
     int64_t ws_bytes;
 };
+
+// ring slots per edge and 32-bit flag words per (pipeline, edge) of the fused backward
+constexpr int kPipeRingSlots = 16;
+constexpr int kPipeFlagWordsPerEdge = 64;
+constexpr int kPipeStatusWordsHead = 64;
 
 MlpSizes make_sizes(const MlpPlan& p, int64_t M);
 

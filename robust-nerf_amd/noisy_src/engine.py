@@ -141,12 +141,19 @@ class GradAllReducer:
         return 1.0 if self.average else 1.0 / self.world
 
     def launch(self, flat: torch.Tensor) -> None:
+        if flat.is_cuda and torch.cuda.is_current_stream_capturing():
+            # inside a hipGraph capture (GraphedTrainer): the stream-ordered form, captured
+            # as the collective's kernel plus the stream dependencies around it
+            self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group)
+            self.pending.append((None, flat))
+            return
         work = self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.pending.append((work, flat))
 
     def finish(self) -> None:
         for work, flat in self.pending:
-            work.wait()
+            if work is not None:
+                work.wait()
             if self.average and self.world > 1:
                 flat.mul_(1.0 / self.world)
         self.pending.clear()
@@ -212,12 +219,16 @@ class GraphedTrainer:
     images, and the two step-dependent Adam scalars come from an 8-byte device pair
     written before each replay (``FusedAdam.device_sched``); the LR schedule and the
     optimizer's step counters advance on the host exactly as in ``Trainer.step``.
-    Single process: the data-parallel all-reduce is not captured."""
+    Data parallel: the trainer's RCCL all-reduces (one per network) are captured inside
+    the graph in their stream-ordered form, so a replay is the whole DP step.
+
+    The graph holds raw device addresses: every network's packed images and pack table
+    and the optimizer's flat m / v buffers.  Those tensors are pinned here, and a replay
+    after any of them was replaced (a checkpoint load, ``FusedAdam.load_state_dict``)
+    raises instead of writing into freed memory."""
 
     def __init__(self, trainer: "Trainer", rays_o: torch.Tensor, rays_d: torch.Tensor, target_rgb: torch.Tensor,
                  t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None, warmup: int = 2):
-        if trainer.reducer is not None:
-            raise ValueError("GraphedTrainer: data-parallel trainers are not captured (use Trainer)")
         self.trainer = trainer
         opt = trainer.optimizer
         if not isinstance(opt, FusedAdam) or len(opt.param_groups) != 1:
@@ -245,6 +256,7 @@ class GraphedTrainer:
         torch.cuda.current_stream(dev).wait_stream(side)
         # capture one step; its host-side bookkeeping (Adam step counters, LR scheduler)
         # ran once without device work, so it is rolled back afterwards
+        self._common_step()
         steps = [(st, st["step"].clone()) for st in self._step_states()]
         sched_state = trainer.scheduler.state_dict()
         lr = [g["lr"] for g in opt.param_groups]
@@ -260,6 +272,30 @@ class GraphedTrainer:
         # the graph holds the pair's address; eager steps between replays (a batch of
         # another shape, see train.train) use the host scalars again
         opt.device_sched = None
+        self._bound = self._bound_buffers()
+
+    def _bound_buffers(self):
+        """The device tensors whose addresses the captured graph holds (strong references)."""
+        nets = [n for n in (self.trainer.model_coarse, self.trainer.model_fine) if n is not None]
+        out = [t for n in nets for t in (n._packed, n._table, n._flat) if t is not None]
+        for m, v in self.trainer.optimizer._flat_state.values():
+            out += [m, v]
+        return out
+
+    def _check_bound(self) -> None:
+        now = self._bound_buffers()
+        if len(now) != len(self._bound) or any(a is not b for a, b in zip(now, self._bound)):
+            raise RuntimeError("GraphedTrainer: a buffer the captured graph writes was replaced (packed images, "
+                               "pack table, parameters or Adam state, e.g. by a checkpoint load); "
+                               "build a new GraphedTrainer")
+
+    def _common_step(self) -> int:
+        """The one Adam step count every buffer shares (one pair of bias corrections
+        drives every span of the captured launch)."""
+        vals = {int(st["step"]) for st in self._step_states()}
+        if len(vals) != 1:
+            raise RuntimeError(f"GraphedTrainer: the optimizer's buffers are at different steps {sorted(vals)}")
+        return vals.pop()
 
     def _step_states(self):
         opt = self.trainer.optimizer
@@ -282,11 +318,12 @@ class GraphedTrainer:
                 if dst is None:
                     raise ValueError("GraphedTrainer: t_rand / u were drawn in the graph at capture")
                 dst.copy_(src)
+        self._check_bound()
         opt = self.trainer.optimizer
         group = opt.param_groups[0]
         b1, b2 = group["betas"]
         states = self._step_states()
-        nxt = int(states[0]["step"]) + 1
+        nxt = self._common_step() + 1
         a, b = ops.adam_sched_values(group["lr"], b1, b2, nxt)
         slot = self._k % len(self._ring_ev)
         if self._ring_ev[slot] is not None:

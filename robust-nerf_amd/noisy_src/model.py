@@ -17,6 +17,7 @@ fp32 (parity) or bf16 MFMA path.
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 from typing import List, Optional, Tuple
 
@@ -51,6 +52,11 @@ class PositionalEncoding(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return ops.positional_encoding(x, self.num_freqs, self.include_input, self.log_sampling)
+
+
+# NR_MLP_BACKWARD=split selects the split dX + dW backward instead of the fused
+# layer-pipelined launch (A/B comparisons; both give bit-identical gradients)
+_SPLIT_BACKWARD = os.environ.get("NR_MLP_BACKWARD", "split") == "split"
 
 
 def _precision_code(p: str) -> int:
@@ -104,9 +110,16 @@ class _MLPFunction(torch.autograd.Function):
         if M > 0:
             ws = torch.empty(int(_hip.load().nr_mlp_workspace_bytes(cfg, M)), device=dev, dtype=torch.uint8)
             st, tag = _hip.stream_ptr(), f"[M={M}]"
-            call("nr_mlp_backward_dx", cfg, ptr(packed), ptr(flat), ptr(xc), ptr(dc) if ctx.has_d else None, M,
-                 ptr(rgb), ptr(sigma), ptr(saved), ptr(g_rgb), ptr(g_sigma), ptr(g_x), ptr(g_d), ptr(ws), st, tag=tag)
-            call("nr_mlp_backward_dw", cfg, M, ptr(saved), ptr(ws), st, tag=tag)
+            args = (cfg, ptr(packed), ptr(flat), ptr(xc), ptr(dc) if ctx.has_d else None, M, ptr(rgb), ptr(sigma),
+                    ptr(saved), ptr(g_rgb), ptr(g_sigma), ptr(g_x), ptr(g_d), ptr(ws), st)
+            if _SPLIT_BACKWARD:
+                # the split form: dX chain (dz images in HBM), then the dW GEMM over them
+                call("nr_mlp_backward_dx", *args, tag=tag)
+                call("nr_mlp_backward_dw", cfg, M, ptr(saved), ptr(ws), st, tag=tag)
+            else:
+                # one layer-pipelined launch (16-bit; the library runs the split form where
+                # the pipeline does not apply, e.g. fp32): bit-identical slabs
+                call("nr_mlp_backward_dxdw", *args, tag=tag)
             call("nr_mlp_backward_reduce", cfg, M, ptr(ws), ptr(gflat), st, tag=tag)
         else:
             gflat.zero_()
@@ -244,7 +257,11 @@ class NeRF(nn.Module):
             nbytes = int(_hip.load().nr_mlp_packed_bytes(cfg))
             if nbytes < 0:
                 raise RuntimeError(f"NeRF config unsupported by the HIP MLP: {_hip.last_error()}")
-            self._packed = torch.empty(nbytes, device=self._flat.device, dtype=torch.uint8)
+            # re-pack into the existing images when they fit: a captured hipGraph
+            # (engine.GraphedTrainer) holds their address, so it stays valid
+            if (self._packed is None or self._packed.numel() != nbytes
+                    or self._packed.device != self._flat.device):
+                self._packed = torch.empty(nbytes, device=self._flat.device, dtype=torch.uint8)
             call("nr_mlp_pack", cfg, ptr(self._flat), ptr(self._packed), _hip.stream_ptr())
             self._packed_key = key
         return self._packed

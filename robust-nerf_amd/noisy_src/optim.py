@@ -12,6 +12,7 @@ synchronisation.  ``FusedAdam`` is a ``torch.optim.Optimizer``, so
 
 from __future__ import annotations
 
+import weakref
 from typing import Iterable, List, Optional, Sequence, Tuple
 
 import torch
@@ -144,6 +145,8 @@ class FusedAdam(torch.optim.Optimizer):
         from .model import flat_owner
         key = tuple(map(id, params))
         plan = self._nerf_plans.get(key)
+        if plan and any(ref() is None for ref, _, _, _ in plan):
+            plan = None  # a network of this plan is gone (its ids may be reused)
         if plan is None:
             plan, i = [], 0
             while i < len(params):
@@ -157,13 +160,17 @@ class FusedAdam(torch.optim.Optimizer):
                 for p in plist:
                     offs.append(off)
                     off += p.numel()
-                plan.append((net, i, i + len(plist), offs))
+                # a weak reference: the cache must not keep a network (and its buffers) alive
+                plan.append((weakref.ref(net), i, i + len(plist), offs))
                 i += len(plist)
             self._nerf_plans[key] = plan
         if not plan:
             return None
         out = []
-        for net, i0, i1, offs in plan:
+        for ref, i0, i1, offs in plan:
+            net = ref()
+            if net is None:
+                return None
             run = params[i0:i1]
             flat, g = net._flat, net._last_gflat
             if flat is None or g is None or run[0].data_ptr() != flat.data_ptr() or g.numel() != flat.numel():
@@ -273,4 +280,11 @@ class FusedAdam(torch.optim.Optimizer):
                         torch.autograd.graph.increment_version(p)
                     if net is not None:  # ... and its images were refreshed in the same launch
                         net._mark_packed_fresh(run)
+        # the step consumed the networks' flat gradients: drop the extra reference, so
+        # zero_grad(set_to_none=True) frees them
+        for plan in self._nerf_plans.values():
+            for ref, _, _, _ in plan or ():
+                net = ref()
+                if net is not None:
+                    net._last_gflat = None
         return loss

@@ -199,8 +199,9 @@ def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
     if process_group is not None:
         rank, world = dist.get_rank(process_group), dist.get_world_size(process_group)
     check_run_args(config, world, train_data, val_data)
-    if graph and world > 1:
-        raise ValueError("train(graph=True) is single-process: the data-parallel all-reduce is not captured")
+    if graph and world > 1 and dist.get_backend(process_group) != "nccl":
+        # the captured step contains the all-reduce: only RCCL collectives are graph-capturable
+        raise ValueError("train(graph=True) with data parallelism needs the nccl (RCCL) backend")
     set_seed(config.train.seed)
     device = config.train.device
     if device.startswith("cuda") and not torch.cuda.is_available():
@@ -286,8 +287,9 @@ def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
             sl = rank_slice(n, rank, world) if world > 1 else slice(0, n)
             args = (batch["rays_o"][sl], batch["rays_d"][sl], batch["target_rgb"][sl],
                     None if t_rand is None else t_rand[sl], None if u is None else u[sl])
-            if graph and graphed is None and iteration >= 1:
-                # captured after one eager step (state exists), on this batch's shape
+            if graph and graphed is None and iteration >= 1 and n == B:
+                # captured after one eager step (state exists), on a full batch: an epoch's
+                # short tail batch would leave every full batch after it eager
                 graphed = GraphedTrainer(trainer, *args, warmup=0)
             if graphed is not None and args[0].shape == graphed.static[0].shape:
                 m = graphed.step(*args)
