@@ -1679,14 +1679,11 @@ __device__ __forceinline__ void tr16(uint64_t& out, uint32_t addr) {
     asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(out) : "v"(addr), "i"(OFF));
 }
 
+// the two 64-bit halves of a transpose-read operand as one bf16x8 (a pure bit cast, so
+// the register allocator can place the two asm outputs as the halves: no copies)
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ bf16x8 tr_pair(uint64_t lo, uint64_t hi) {
-    bf16x8 r;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        r[j] = __builtin_bit_cast(__bf16, static_cast<unsigned short>(lo >> (16 * j)));
-        r[4 + j] = __builtin_bit_cast(__bf16, static_cast<unsigned short>(hi >> (16 * j)));
-    }
-    return r;
+    return __builtin_bit_cast(bf16x8, u64x2_t{lo, hi});
 }
 
 // LDS byte offsets, within a staged block, of the two transpose reads that give
@@ -2532,7 +2529,6 @@ bool pipe_layout(const MlpPlan& p, const MlpSizes& z, PipeArgs& a, int& NX) {
             st.out_edge = n;
             st.out_ncons = 1;
             st.job = jdir;
-            st.job2 = jfeat;
             st.mask_layer = n;
             st.w_img = p.lin[n + 1].pk_bwdr;
             st.ws_store[0] = z.ws_off[p.ws_dir];
@@ -2563,6 +2559,7 @@ bool pipe_layout(const MlpPlan& p, const MlpSizes& z, PipeArgs& a, int& NX) {
                 st.ws_store[x] = z.ws_off[WS_DZ0 + xl[x]];
             }
             st.job = 0;
+            st.job2 = jfeat;
             st.sv_in = z.saved_off[SV_XENC];
         }
     }
@@ -3129,7 +3126,7 @@ int nr_mlp_backward_dxdw(const NrMlpConfig* cfg, const void* packed, const float
     a.npipe = z.chunks;
     const int cus = device_cus();
     bool launched = false;
-    if (layout && cus > 0 && a.npipe * a.nstage <= cus) {
+    if (layout && cus > 0 && a.npipe * a.nstage <= cus && M <= kPipeMaxM) {
         char* ws = static_cast<char*>(workspace);
         a.packed = static_cast<const char*>(packed);
         a.saved = static_cast<const char*>(saved);
@@ -3187,7 +3184,7 @@ int nr_mlp_backward_pipelined(const NrMlpConfig* cfg, int64_t M) {
     int NX = 0;
     if (!pipe_layout(p, z, a, NX)) return 0;
     const int cus = device_cus();
-    return cus > 0 && z.chunks * (p.n_layers + 2) <= cus ? 1 : 0;
+    return cus > 0 && z.chunks * (p.n_layers + 2) <= cus && M <= kPipeMaxM ? 1 : 0;
 }
 
 int64_t nr_mlp_pipe_status_offset(const NrMlpConfig* cfg, int64_t M) {

@@ -152,9 +152,13 @@ struct MlpSizes {
 };
 
 // ring slots per edge and 32-bit flag words per (pipeline, edge) of the fused backward
-constexpr int kPipeRingSlots = 16;
-constexpr int kPipeFlagWordsPerEdge = 64;
+constexpr int kPipeRingSlots = 32;
+constexpr int kPipeFlagWordsPerEdge = 128;
+#ifdef NR_PIPE_PROF
+constexpr int kPipeStatusWordsHead = 64 + 512 * 32;  // + per-workgroup timing records (diagnostic builds)
+#else
 constexpr int kPipeStatusWordsHead = 64;
+#endif
 
 MlpSizes make_sizes(const MlpPlan& p, int64_t M);
 

@@ -9,7 +9,7 @@ timeout -k 10 400 python -u -m pytest tests/test_pipe.py -m gpu -v -p no:cachepr
 rc=$?
 tail -25 gpurun_out/r04_pipe_pytest.log
 if [ $rc -ne 0 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
-timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline > gpurun_out/r04_pipe_bench.json 2> gpurun_out/r04_pipe_bench.err
+NR_MLP_BACKWARD=fused timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline > gpurun_out/r04_pipe_bench.json 2> gpurun_out/r04_pipe_bench.err
 rc=$?
 if [ $rc -ne 0 ]; then echo "bench rc=$rc"; tail -20 gpurun_out/r04_pipe_bench.err; exit $rc; fi
 python -c "import json;d=json.load(open('gpurun_out/r04_pipe_bench.json'));print(d['value'], d['ms_per_step'], d['kernel_ms'])"
