@@ -443,6 +443,12 @@ def main():
     if args.warmup is None:
         args.warmup = 2 if args.eval else 20
 
+    # stdout carries exactly ONE line, the JSON record: anything else written to fd 1 (the
+    # RCCL init banner, library chatter) goes to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -473,7 +479,7 @@ def main():
     if args.eval:
         out = eval_bench(args, dev, world, rank, pg)
         if rank == 0:
-            print(json.dumps(out))
+            print(json.dumps(out), file=json_out, flush=True)
         if pg is not None:
             torch.distributed.destroy_process_group()
         return
@@ -675,7 +681,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.pose_opt:
         out["cpu_baseline"] = cpu_baseline(steps=args.cpu_steps)
     if rank == 0:
-        print(json.dumps(out))
+        print(json.dumps(out), file=json_out, flush=True)
     if pg is not None:
         torch.distributed.destroy_process_group()
 
