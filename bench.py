@@ -224,23 +224,30 @@ def pose_opt_setup(H: int, W: int, device):
 
 
 def psnr_record():
-    """The latest committed test-PSNR record (profiles/r*_psnr_parity.json, written by
-    tests/psnr_parity.py on the GPU box): RECORDED, not measured in this run."""
-    recs = sorted((ROOT / "profiles").glob("r*_psnr_parity.json"))
-    if not recs:
-        return None
-    f = recs[-1]
-    rec = json.loads(f.read_text())
-    if "summary" not in rec:
-        return None
-    return {"recorded": True, "source": f"profiles/{f.name} (tests/psnr_parity.py)",
-            "commit": rec.get("commit"), "scene": rec.get("scene", "analytic 3-sphere scene, lego train cameras"),
-            "iters": rec["iters"], "seeds": rec["seeds"],
-            "mean_db": {k: round(v["mean"], 3) for k, v in rec["summary"].items()},
-            "lr_decay": rec.get("lr_decay"),
-            "paired_delta_db_vs_ref": {k: v.get("paired_mean_db", v["delta_mean_db"])
-                                       for k, v in rec["delta_vs_ref"].items()},
-            "paired_se_db": {k: v.get("paired_se_db", v["se_of_delta_db"]) for k, v in rec["delta_vs_ref"].items()}}
+    """The latest committed test-PSNR records (profiles/r*_psnr_parity*.json, written by
+    tests/psnr_parity.py on the GPU box): RECORDED, not measured in this run.  The main
+    one anneals the LR (lr_decay = 1: paired differences resolve to a few hundredths of a
+    dB); `reference_schedule` is the reference's own LambdaLR (lr_decay = 250,
+    train.py:405-411), under which equal-iteration runs stay chaotic."""
+    def one(f):
+        rec = json.loads(f.read_text())
+        if "summary" not in rec:
+            return None
+        return {"recorded": True, "source": f"profiles/{f.name} (tests/psnr_parity.py)",
+                "commit": rec.get("commit"), "scene": rec.get("scene", "analytic 3-sphere scene, lego train cameras"),
+                "iters": rec["iters"], "seeds": rec["seeds"],
+                "mean_db": {k: round(v["mean"], 3) for k, v in rec["summary"].items()},
+                "lr_decay": rec.get("lr_decay"),
+                "paired_delta_db_vs_ref": {k: v.get("paired_mean_db", v["delta_mean_db"])
+                                           for k, v in rec["delta_vs_ref"].items()},
+                "paired_se_db": {k: v.get("paired_se_db", v["se_of_delta_db"]) for k, v in rec["delta_vs_ref"].items()}}
+    recs = [(f, json.loads(f.read_text()).get("lr_decay")) for f in sorted((ROOT / "profiles").glob("r*_psnr_parity*.json"))]
+    main = [f for f, ld in recs if ld in (1, None)]
+    ref = [f for f, ld in recs if ld == 250]
+    out = one(main[-1]) if main else None
+    if out is not None and ref:
+        out["reference_schedule"] = one(ref[-1])
+    return out
 
 
 def _cpu_model() -> str:
