@@ -1670,6 +1670,10 @@ __device__ __forceinline__ int dw_feat(int r) { return acc_row(r & 15, r >> 4); 
 // dw_frag_bf16 bank-conflict free (the 16 slots a 32-lane half reads are
 // distinct mod 16).  glds writes lane-linear, so the swizzle goes on the source.
 __device__ __forceinline__ int dw_slot(int L, int s) { return L ^ (((L >> 5) & 1) << 2) ^ (s << 3); }
+// fp32 staging: fragment f's 16-B chunk c lands at chunk position c ^ 2 (f + 4 (c >> 5))
+// (an involution: bits 1-3 only), so the per-sample reads of mlp_dw_kernel's fp32 path
+// spread over all 16 four-bank groups instead of 2 (8-way conflicts)
+__device__ __forceinline__ int dw_slot32(int L, int f) { return L ^ (2 * (f + 4 * ((L >> 5) & 1))); }
 
 // ds_read_b64_tr_b16 through inline asm: the builtin makes hipcc wait vmcnt(0)
 // (every in-flight LDS-DMA stage) before each read, which would serialise the
@@ -1682,6 +1686,12 @@ __device__ __forceinline__ void tr16(uint64_t& out, uint32_t addr) {
 // the two 64-bit halves of a transpose-read operand as one bf16x8 (a pure bit cast, so
 // the register allocator can place the two asm outputs as the halves: no copies)
 typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+// ds_read_b32 through inline asm (as tr16: no compiler drain of in-flight LDS-DMA)
+template <int OFF>
+__device__ __forceinline__ void ds_rd32(float& out, uint32_t addr) {
+    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(out) : "v"(addr), "i"(OFF));
+}
+
 __device__ __forceinline__ bf16x8 tr_pair(uint64_t lo, uint64_t hi) {
     return __builtin_bit_cast(bf16x8, u64x2_t{lo, hi});
 }
@@ -1766,7 +1776,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
             int sg = 0, p0 = 0;
             while (pc >= p0 + a.seg_blocks[j][sg] * FPB) p0 += a.seg_blocks[j][sg++] * FPB;
             const int nb = a.seg_blocks[j][sg];
-            const int L = k16<PREC> ? dw_slot(lane, (pc - p0) % FPB) : lane;
+            const int L = k16<PREC> ? dw_slot(lane, (pc - p0) % FPB) : dw_slot32(lane, (pc - p0) % FPB);
             pstride[k] = static_cast<int64_t>(nb) * BLK;
             psrc[k] = a.seg_ptr[j][sg] + t0 * pstride[k] + (pc - p0) * kFragBytes + L * 16;
             pdst[k] = pad ? -1 : pc * kFragBytes;
@@ -1811,6 +1821,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     // the share's np x nq blocks run as the next compiled shape up, the extra blocks
     // accumulate garbage that is never written; fp32: kDwMaxP x kDwMaxQ with runtime
     // validity).  Each shape's accumulators live only inside its own instantiation.
+    using std::integral_constant;
     auto run = [&](auto npc, auto nqc) {
         constexpr int NP = decltype(npc)::value, NQ = decltype(nqc)::value;
         f32x16 acc[NP][NQ];
@@ -1882,30 +1893,52 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
                         for (int p = 0; p < NP; ++p) bsum[p] = dw_acc4<PREC>(ra[p][1], dw_acc4<PREC>(ra[p][0], bsum[p]));
                 }
             } else {
-                // fp32 image [tq][L][4]: operand row r <-> (hh = r>>4, reg i = r&15 -> frag i>>2, elem i&3)
+                // fp32 image [tq][L][4]: operand row r <-> (hh = r>>4, reg i = r&15 -> frag i>>2,
+                // elem i&3); sample m = 2 ss + kk is 16-B chunk 32 hh + m of the fragment,
+                // staged at chunk position 32 hh + 2 (ss ^ k2) + kk (dw_slot32, k2 = frag + 4 hh):
+                // the 16 chunks one read instruction touches fall in 16 distinct 4-bank groups
                 const int r = lane & 31, kk = lane >> 5;
                 const int hh = r >> 4, i = r & 15;
-                const int off = ((i >> 2) * 64 + 32 * hh) * 16 + (i & 3) * 4;
-#pragma unroll 4
-                for (int ss = 0; ss < 16; ++ss) {
-                    const int m = 2 * ss + kk;
-                    float A[NP], Bv[NQ];
+                const int k2 = (i >> 2) + 4 * hh;
+                const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf)) +
+                                      ((i >> 2) * 64 + 32 * hh + kk) * 16 + (i & 3) * 4;
+                const uint32_t bufA = base + row0 * BLK, bufB = base + (NBz + col0) * BLK;
+                const uint32_t kx = static_cast<uint32_t>(k2) << 5;
+                // operands through asm reads (a plain LDS load makes the compiler drain every
+                // in-flight staging DMA first), one sample pair read ahead; the compiled
+                // share shape runs branch-free (blocks past np x nq accumulate garbage that
+                // is never written, as in the 16-bit path)
+                float Ar[2][NP], Br[2][NQ];
+                auto rd = [&](auto sc) {
+                    constexpr int ss = decltype(sc)::value;
+                    // (ss ^ k2) << 5 computed in place: sixteen hoisted per-lane offsets would
+                    // cost sixteen registers across the tile loop
+                    uint32_t o;
+                    asm volatile("v_xor_b32 %0, %1, %2" : "=v"(o) : "i"(ss << 5), "v"(kx));
+                    const uint32_t oa = bufA + o, ob = bufB + o;
+                    rbm_static_for<NP>([&](auto pp) { ds_rd32<decltype(pp)::value * BLK>(Ar[ss & 1][decltype(pp)::value], oa); });
+                    rbm_static_for<NQ>([&](auto qq) { ds_rd32<decltype(qq)::value * BLK>(Br[ss & 1][decltype(qq)::value], ob); });
+                };
+                rd(integral_constant<int, 0>{});
+                rbm_static_for<16>([&](auto sc) {
+                    constexpr int ss = decltype(sc)::value;
+                    if constexpr (ss + 1 < 16) {
+                        rd(integral_constant<int, ss + 1>{});
+                        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NP + NQ) : "memory");
+                    } else {
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    }
 #pragma unroll
-                    for (int p = 0; p < NP; ++p)
-                        A[p] = nval[p] ? *reinterpret_cast<const float*>(buf + (row0 + p) * BLK + off + m * 16) : 0.f;
+                    for (int p = 0; p < NP; ++p) asm volatile("" : "+v"(Ar[ss & 1][p]));
 #pragma unroll
-                    for (int q = 0; q < NQ; ++q)
-                        Bv[q] = kval[q] ? *reinterpret_cast<const float*>(buf + (NBz + col0 + q) * BLK + off + m * 16)
-                                        : 0.f;
+                    for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(Br[ss & 1][q]));
 #pragma unroll
                     for (int p = 0; p < NP; ++p) {
-                        if (!nval[p]) continue;
-                        if (do_bias) bsum[p] += A[p];
+                        bsum[p] += Ar[ss & 1][p];  // summed by every wave, written by the bias share's
 #pragma unroll
-                        for (int q = 0; q < NQ; ++q)
-                            if (kval[q]) acc[p][q] = mfma_f32(A[p], Bv[q], acc[p][q]);
+                        for (int q = 0; q < NQ; ++q) acc[p][q] = mfma_f32(Ar[ss & 1][p], Br[ss & 1][q], acc[p][q]);
                     }
-                }
+                });
             }
         }
         if (!active) return;
@@ -1929,7 +1962,6 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
             }
         }
     };
-    using std::integral_constant;
     if constexpr (k16<PREC> && !NR_DW_ONESHAPE) {
         // compiled shares: 1x2, 4x1, 4x2, 5x2 (a smaller share runs the next one up)
         if (np <= 1)
