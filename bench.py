@@ -51,7 +51,9 @@ DW_FEATURES = (63 + 8 * 256 + 256 + 27 + 128) + (8 * 256 + 256 + 128 + 1 + 3)
 # kernels behind each entry point (16-bit forward / dX: the row-block-major kernels)
 KERNEL_OF = {"nr_mlp_forward": ("mlp_fwd_rbm_kernel", "mlp_fwd_kernel"),
              "nr_mlp_backward_dx": ("mlp_bwd_rbm_kernel", "mlp_bwd_kernel"),
-             "nr_mlp_backward_dw": ("mlp_dw_kernel",), "nr_mlp_backward_reduce": ("mlp_dw_reduce_kernel",)}
+             "nr_mlp_backward_dw": ("mlp_dw_kernel",), "nr_mlp_backward_reduce": ("mlp_dw_reduce_kernel",),
+             # opt-in fused layer-pipelined backward (NR_MLP_BACKWARD=fused, csrc/mlp_pipe.inc)
+             "nr_mlp_backward_dxdw": ("mlp_bwd_pipe_kernel",)}
 
 
 def traffic_of(kernels, M: int, prec: str):
@@ -538,7 +540,8 @@ def main():
     # every fused-MLP entry point is timed over the last warm-up steps (kernel_ms) to find
     # the dominant kernel; inside the timed region only that kernel's launches carry HIP
     # events (each bracketed call costs a few us of queue gap)
-    mlp_entries = ["nr_mlp_forward", "nr_mlp_backward_dx", "nr_mlp_backward_dw", "nr_mlp_backward_reduce"]
+    mlp_entries = ["nr_mlp_forward", "nr_mlp_backward_dx", "nr_mlp_backward_dw", "nr_mlp_backward_dxdw",
+                   "nr_mlp_backward_reduce"]
     wtimer = _hip.CallTimer(mlp_entries)
     for k in range(args.warmup):
         if k == args.warmup // 2:

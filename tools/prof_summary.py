@@ -30,7 +30,8 @@ ROOT = Path(__file__).resolve().parents[1]
 FAMILIES = {"mlp_fwd_kernel": "nr_mlp_forward", "mlp_bwd_kernel": "nr_mlp_backward_dx",
             "mlp_fwd_rbm_kernel": "nr_mlp_forward", "mlp_bwd_rbm_kernel": "nr_mlp_backward_dx",
             "mlp_dinput_kernel": "nr_mlp_backward_dx (input grads)",
-            "mlp_dw_kernel": "nr_mlp_backward_dw", "mlp_dw_reduce_kernel": "nr_mlp_backward_reduce"}
+            "mlp_dw_kernel": "nr_mlp_backward_dw", "mlp_dw_reduce_kernel": "nr_mlp_backward_reduce",
+            "mlp_bwd_pipe_kernel": "nr_mlp_backward_dxdw"}
 
 
 def source_hash() -> str:
@@ -61,7 +62,7 @@ def sample_count(name: str, grid: int, last_M: int) -> int:
     fam = short(name)
     if fam in ("mlp_fwd_kernel", "mlp_bwd_kernel", "mlp_fwd_rbm_kernel", "mlp_bwd_rbm_kernel"):
         return grid // 64 * 32
-    if fam in ("mlp_dw_kernel", "mlp_dw_reduce_kernel", "mlp_dinput_kernel"):
+    if fam in ("mlp_dw_kernel", "mlp_dw_reduce_kernel", "mlp_dinput_kernel", "mlp_bwd_pipe_kernel"):
         return last_M
     return 0
 
