@@ -1962,7 +1962,12 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
             }
         }
     };
-    if constexpr (k16<PREC> && !NR_DW_ONESHAPE) {
+    if constexpr (!k16<PREC> && !NR_DW_ONESHAPE) {
+        // fp32: the plan keeps every share within 4 x 2 (the sigma head is its own job), so
+        // one compiled 4x2 share: a wave pair on one SIMD runs 16 blocks per tile of an
+        // h-job instead of the 20 of the 5x2 shape (a second shape in the kernel spills)
+        run(integral_constant<int, 4>{}, integral_constant<int, kDwMaxQ>{});
+    } else if constexpr (k16<PREC> && !NR_DW_ONESHAPE) {
         // compiled shares: 1x2, 4x1, 4x2, 5x2 (a smaller share runs the next one up)
         if (np <= 1)
             run(integral_constant<int, 1>{}, integral_constant<int, 2>{});

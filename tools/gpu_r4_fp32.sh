@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_parity_mlp.py tests/test_parity_fullsize.py -m gpu -k "fp32" -q \
+timeout -k 10 600 python -u -m pytest tests/test_parity_mlp.py tests/test_parity_fullsize.py tests/test_fused_optim.py -m gpu -k "fp32 or plan or model" -q \
   -p no:cacheprovider -x --timeout 300 --timeout-method thread > gpurun_out/r04_fp32_pytest.log 2>&1
 rc=$?
 tail -4 gpurun_out/r04_fp32_pytest.log
