@@ -178,12 +178,10 @@ __device__ __forceinline__ void pe_feat_bwd(float x0, float x1, float x2, int f,
         const float v = fr * xv;
         d = rem < 3 ? (g * cosf(v)) * fr : (g * -sinf(v)) * fr;
     }
-    if (c == 0)
-        g0 += d;
-    else if (c == 1)
-        g1 += d;
-    else
-        g2 += d;
+    // selects, not branches: the branches became a run-time-indexed scratch array
+    g0 += c == 0 ? d : 0.f;
+    g1 += c == 1 ? d : 0.f;
+    g2 += c == 2 ? d : 0.f;
 }
 
 // bf16 positional encoding.  sin/cos by the hardware v_sin_f32 (argument in
@@ -276,11 +274,13 @@ __device__ __forceinline__ float pe_fast(const PeRev& p, int f0, int f1, bool h1
 __device__ __forceinline__ void pe_fast_bwd(const PeRev& p, int f0, int f1, bool h1, int L, float g, float& g0,
                                             float& g1, float& g2) {
     auto chan = [](int f) { return f < 3 ? f : ((f - 3) - 6 * ((f - 3) / 6)) % 3; };
+    // selects: a run-time index into p.hi / p.lo put them in scratch
+    auto sel = [](const float (&v)[3], int c) { return c == 0 ? v[0] : (c == 1 ? v[1] : v[2]); };
     auto live = [&](int f) { return f < 3 || (f - 3) / 6 < L; };
     auto dgamma = [&](int f) -> float {  // d gamma_f / d x_c (f >= 3, live)
         const int fp = f - 3, k = fp / 6, rem = fp - 6 * k, c = rem % 3;
         const float sc = static_cast<float>(1 << (k < 24 ? k : 0));
-        const float hi = p.hi[c] * sc, lo = fmaf(p.lo[c], sc, rem < 3 ? 0.25f : 0.5f);
+        const float hi = sel(p.hi, c) * sc, lo = fmaf(sel(p.lo, c), sc, rem < 3 ? 0.25f : 0.5f);
         return __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(hi) + lo) * sc;
     };
     float d;
@@ -288,8 +288,8 @@ __device__ __forceinline__ void pe_fast_bwd(const PeRev& p, int f0, int f1, bool
         const int fp0 = f0 - 3, k0 = fp0 / 6, r0 = fp0 - 6 * k0;
         const int fp1 = f1 - 3, k1 = fp1 / 6, r1 = fp1 - 6 * k1;
         const float s0 = static_cast<float>(1 << (k0 < 24 ? k0 : 0)), s1 = static_cast<float>(1 << (k1 < 24 ? k1 : 0));
-        const float hi = h1 ? p.hi[r1 % 3] * s1 : p.hi[r0 % 3] * s0;
-        const float lo = h1 ? fmaf(p.lo[r1 % 3], s1, r1 < 3 ? 0.25f : 0.5f) : fmaf(p.lo[r0 % 3], s0, r0 < 3 ? 0.25f : 0.5f);
+        const float hi = h1 ? sel(p.hi, r1 % 3) * s1 : sel(p.hi, r0 % 3) * s0;
+        const float lo = h1 ? fmaf(sel(p.lo, r1 % 3), s1, r1 < 3 ? 0.25f : 0.5f) : fmaf(sel(p.lo, r0 % 3), s0, r0 < 3 ? 0.25f : 0.5f);
         d = g * (__builtin_amdgcn_sinf(__builtin_amdgcn_fractf(hi) + lo) * (h1 ? s1 : s0));
     } else {
         const float a0 = f0 < 3 ? 1.f : (live(f0) ? dgamma(f0) : 0.f);
@@ -705,6 +705,26 @@ __device__ __forceinline__ void lgkm_wait_pair(int n, bf16x8& a0, bf16x8& a1) {
     }
 }
 
+// fp32 A operands: the four 1-KB fragments of one row block, read by asm
+__device__ __forceinline__ void ds_read_quad(f32x4 (&dst)[4], uint32_t addr) {
+    asm volatile("ds_read_b128 %0, %1" : "=v"(dst[0]) : "v"(addr));
+    asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(dst[1]) : "v"(addr));
+    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(dst[2]) : "v"(addr));
+    asm volatile("ds_read_b128 %0, %1 offset:3072" : "=v"(dst[3]) : "v"(addr));
+}
+__device__ __forceinline__ void lgkm_wait_one(int n, f32x4& a) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a)); break;
+        case 1: asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(a)); break;
+        case 2: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a)); break;
+        case 3: asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a)); break;
+        case 4: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a)); break;
+        case 5: asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(a)); break;
+        case 6: asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(a)); break;
+        default: asm volatile("s_waitcnt lgkmcnt(7)" : "+v"(a)); break;
+    }
+}
+
 // Epilogue hooks of stream_gemm's last chunk (16-bit, one tile per wave): as the
 // MFMAs of row block r issue, the bias MFMA of block r-1 and the packing / ReLU /
 // mask bits / LDS store of block r-2 run, so the layer epilogue overlaps the
@@ -793,9 +813,13 @@ __device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1]
         bf16x8 aring[PF + 1][2];
         const uint32_t abase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(slot)) +
                                static_cast<uint32_t>(nb0 * kFPB<PREC> * kFragBytes);
-        if constexpr (k16<PREC>)
+        f32x4 aq[2][4];  // fp32: row block r + 1 is read while row block r multiplies
+        if constexpr (k16<PREC>) {
 #pragma unroll
             for (int r = 0; r < PF; ++r) ds_read_pair(aring[r], abase + r * 2 * kFragBytes);
+        } else if constexpr (NR_APF > 0) {
+            ds_read_quad(aq[0], abase);
+        }
         if constexpr (B_ASM)
 #pragma unroll
             for (int t = 0; t < TPW; ++t) lgkm_wait_pair(2 * PF + 2 * (TPW - 1 - t), in[t].s[0], in[t].s[1]);
@@ -832,9 +856,17 @@ __device__ __forceinline__ void stream_gemm(f32x16 (&acc1)[TPW][N1 > 0 ? N1 : 1]
                     }
                 }
             } else {
+                if constexpr (NR_APF > 0)
+                    if (r + 1 < NRB) ds_read_quad(aq[(r + 1) & 1], abase + (r + 1) * 4 * kFragBytes);
 #pragma unroll
                 for (int tq = 0; tq < 4; ++tq) {
-                    const f32x4 a = *reinterpret_cast<const f32x4*>(fp + tq * kFragBytes);
+                    f32x4 a;
+                    if constexpr (NR_APF > 0) {
+                        a = aq[r & 1][tq];
+                        lgkm_wait_one((r + 1 < NRB ? 4 : 0) + 3 - tq, a);
+                    } else {
+                        a = *reinterpret_cast<const f32x4*>(fp + tq * kFragBytes);
+                    }
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -978,9 +1010,16 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
                         v[r] = (k16<PREC> && NR_FASTPE)
                                    ? pe_fast(pr, 32 * kb + acc_row(r, 0), 32 * kb + acc_row(r, 1), h != 0, a.L)
                                    : pe_feat(p0, p1, p2, 32 * kb + acc_row(r, h), a.L);
-                    to_in<PREC>(v, xe.v[t][kb]);
+                    InBlk<PREC> o;
+                    to_in<PREC>(v, o);
                     if constexpr (TRAIN)
-                        if (tok[t]) store_img<PREC>(a.saved + a.sv_off[SV_XENC], tile0 + t, XB, kb, xe.v[t][kb], lane);
+                        if (tok[t]) store_img<PREC>(a.saved + a.sv_off[SV_XENC], tile0 + t, XB, kb, o, lane);
+                    // constant indices: the fp32 body (accurate sinf) is too big for the
+                    // pragma to unroll, and a run-time index put xe in scratch, whose
+                    // reloads in the stream then drained the in-flight weight DMA
+#pragma unroll
+                    for (int k2 = 0; k2 < XB; ++k2)
+                        if (k2 == kb) xe.v[t][k2] = o;
                 }
             }
             bool hooked = false;
