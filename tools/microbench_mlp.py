@@ -38,5 +38,7 @@ def bench(prec, M, reps=int(__import__("os").environ.get("MB_REPS", "20"))):
         out[name] = ms
         print(f"{prec} M={M} {name:10s} {ms:8.3f} ms  {tf:7.1f} TF/s-equiv")
     return out
+# MB_M: comma-separated sample counts (default the cfg #2 fine net)
 for prec in sys.argv[1:] or ["bf16"]:
-    bench(prec, 786432)
+    for M in [int(v) for v in __import__("os").environ.get("MB_M", "786432").split(",")]:
+        bench(prec, M)
