@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Ran against the NR_RBM_WAVES patch of DESIGN.md section 9 item 7, since reverted: the
+#  variant libraries it names no longer build from this tree.)
 # Row-block-major kernels at 4 vs 8 waves per workgroup: microbench over launch sizes
 # (forced-4 / forced-8 variant libraries), the MLP parity tests on the forced-4 build,
 # then the default (size-selected) library's tests and 512-ray / cfg #2 bench lines.

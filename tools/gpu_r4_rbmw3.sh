@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Ran against the NR_RBM_WAVES patch of DESIGN.md section 9 item 7, since reverted: the
+#  variant libraries it names no longer build from this tree.)
 # Same-box A/B of the 512-ray graph-replayed step: size-selected wave count (default
 # library) vs forced 8 waves (variant rbm8), alternating, two runs each.
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
