@@ -94,14 +94,15 @@ __global__ void sample_pdf_kernel(const float* bins_g, const float* w_g, const f
     }
 }
 
-template <int KP>  // ceil((Nc + Nf) / 64): sort entries per lane
 __global__ void sample_hier_kernel(const float* ro, const float* rd, const float* zc_g, const float* wc_g,
                                    const float* u_g, int B, int Nc, int Nf, float* zf_out, float* pts_out) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int b = blockIdx.x * kRaysPerBlock + wv;
     const int Nb = Nc - 1, T = Nc + Nf;
-    float* bins = smem + wv * (3 * Nb + T);
+    int P2 = 1;  // the sort's padded length (below)
+    while (P2 < T) P2 <<= 1;
+    float* bins = smem + wv * (3 * Nb + P2);
     float* cdf = bins + Nb;
     float* wbuf = cdf + Nb;
     float* uni = wbuf + Nb;
@@ -125,21 +126,24 @@ __global__ void sample_hier_kernel(const float* ro, const float* rd, const float
     }
     __syncthreads();
     if (!live) return;
-    // all-pairs rank sort of uni[0..T): rank = #{q: x_q < x} + #{q < e: x_q == x}
-    float v[KP];
-    int rank[KP];
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-        const int e = lane + 64 * k;
-        v[k] = e < T ? uni[e] : 0.f;
-        rank[k] = 0;
-    }
-    for (int q = 0; q < T; ++q) {
-        const float x = uni[q];
-#pragma unroll
-        for (int k = 0; k < KP; ++k) {
-            const int e = lane + 64 * k;
-            rank[k] += (x < v[k]) || (x == v[k] && q < e);
+    // bitonic sort of uni[0..T), padded with +inf to P = 2^ceil(log2 T), in the wave's
+    // LDS (only the values leave the sort, as in torch.sort(...)[0], so the order among
+    // equal values cannot show).  An all-pairs rank sort cost T^2 compares per ray.
+    const int P = P2;
+    for (int e = T + lane; e < P; e += 64) uni[e] = __builtin_inff();
+    __builtin_amdgcn_wave_barrier();
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = lane; t < (P >> 1); t += 64) {
+                const int lo = ((t & ~(j - 1)) << 1) | (t & (j - 1)), hi = lo + j;
+                const float x = uni[lo], y = uni[hi];
+                const bool swap = (lo & k) == 0 ? (x > y) : (x < y);
+                if (swap) {
+                    uni[lo] = y;
+                    uni[hi] = x;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
         }
     }
     const int64_t ob = static_cast<int64_t>(b) * T;
@@ -148,17 +152,14 @@ __global__ void sample_hier_kernel(const float* ro, const float* rd, const float
         ox = ro[3 * b], oy = ro[3 * b + 1], oz = ro[3 * b + 2];
         dx = rd[3 * b], dy = rd[3 * b + 1], dz = rd[3 * b + 2];
     }
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-        const int e = lane + 64 * k;
-        if (e < T) {
-            const int64_t o = ob + rank[k];
-            zf_out[o] = v[k];
-            if (pts_out) {
-                pts_out[3 * o] = ox + dx * v[k];
-                pts_out[3 * o + 1] = oy + dy * v[k];
-                pts_out[3 * o + 2] = oz + dz * v[k];
-            }
+    for (int e = lane; e < T; e += 64) {
+        const float v = uni[e];
+        const int64_t o = ob + e;
+        zf_out[o] = v;
+        if (pts_out) {
+            pts_out[3 * o] = ox + dx * v;
+            pts_out[3 * o + 1] = oy + dy * v;
+            pts_out[3 * o + 2] = oz + dz * v;
         }
     }
 }
@@ -188,15 +189,12 @@ int nr_sample_hierarchical(const float* ro, const float* rd, const float* zc, co
     NR_REQUIRE(Nc + Nf <= 64 * kMaxPerLane, "nr_sample_hierarchical: Nc+Nf=%d exceeds %d", Nc + Nf,
                64 * kMaxPerLane);
     if (B == 0) return NR_OK;
-    const size_t lds = sizeof(float) * kRaysPerBlock * (3 * (Nc - 1) + Nc + Nf);
+    int P2 = 1;  // the kernel's sort pads Nc + Nf to a power of two
+    while (P2 < Nc + Nf) P2 <<= 1;
+    const size_t lds = sizeof(float) * kRaysPerBlock * (3 * (Nc - 1) + P2);
     const dim3 grid(ceil_div(B, kRaysPerBlock)), block(64 * kRaysPerBlock);
     const hipStream_t st = static_cast<hipStream_t>(stream);
-    switch ((Nc + Nf + 63) / 64) {
-#define NR_HIER(K) \
-    case K: hipLaunchKernelGGL(sample_hier_kernel<K>, grid, block, lds, st, ro, rd, zc, wc, u, B, Nc, Nf, zf, pts); break;
-        NR_HIER(1) NR_HIER(2) NR_HIER(3) NR_HIER(4) NR_HIER(5) NR_HIER(6) NR_HIER(7) NR_HIER(8)
-#undef NR_HIER
-    }
+    hipLaunchKernelGGL(sample_hier_kernel, grid, block, lds, st, ro, rd, zc, wc, u, B, Nc, Nf, zf, pts);
     NR_LAUNCH_CHECK("nr_sample_hierarchical");
     return NR_OK;
 }
