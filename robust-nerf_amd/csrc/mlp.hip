@@ -2037,47 +2037,46 @@ struct ReduceArgs {
     int job_KB[kMaxJobs];
 };
 
+// One workgroup per (reduce range k = blockIdx.y, output row r = blockIdx.x): the row's
+// weight columns and its bias (column `in`) across the threads, so neither an index
+// search per parameter nor a division; consecutive columns read consecutive slab floats.
 __global__ void mlp_dw_reduce_kernel(ReduceArgs a) {
-    // 32-bit index math: a parameter index and its offset inside a range fit easily
-    // (64-bit division made the index walk dominate this memory-bound kernel)
-    const int pidx = static_cast<int>(blockIdx.x) * static_cast<int>(blockDim.x) + static_cast<int>(threadIdx.x);
-    if (pidx >= a.param_count) return;
-    int job = -1, row = 0, col = 0;
-    for (int k = 0; k < a.n_red && job < 0; ++k) {
-        const int w_off = static_cast<int>(a.w_off[k]), b_off = static_cast<int>(a.b_off[k]);
-        const int wsz = a.rows[k] * a.in[k];
-        if (pidx >= w_off && pidx < w_off + wsz) {
-            const unsigned e = static_cast<unsigned>(pidx - w_off);
-            const int r = static_cast<int>(e / static_cast<unsigned>(a.in[k]));
-            const int c = static_cast<int>(e - static_cast<unsigned>(r) * static_cast<unsigned>(a.in[k]));
-            for (int s = 0; s < a.nseg[k]; ++s) {
-                const RedSeg& sg = a.seg[k][s];
+    const int k = blockIdx.y, r = blockIdx.x;
+    if (r >= a.rows[k]) return;
+    const int in = a.in[k];
+    const int64_t st = a.slab_floats_per_chunk;
+    for (int c = threadIdx.x; c <= in; c += blockDim.x) {
+        int job = -1, row = 0, col = 0;
+        int64_t dst;
+        if (c < in) {
+            for (int q = 0; q < a.nseg[k]; ++q) {
+                const RedSeg& sg = a.seg[k][q];
                 if (c >= sg.col0 && c < sg.col0 + sg.width) {
                     job = sg.job;
                     row = sg.slab_row0 + r;
                     col = sg.slab_col0 + (c - sg.col0);
                 }
             }
-            if (job < 0) return;
-        } else if (pidx >= b_off && pidx < b_off + a.rows[k]) {
+            dst = a.w_off[k] + static_cast<int64_t>(r) * in + c;
+        } else {
             job = a.bjob[k];
-            row = a.brow0[k] + (pidx - b_off);
+            row = a.brow0[k] + r;
             col = a.job_KB[job] * 32;
+            dst = a.b_off[k] + r;
         }
+        if (job < 0) continue;
+        const int ld = a.job_KB[job] * 32 + 1;
+        const float* s = a.slabs + a.job_slab[job] + static_cast<int64_t>(row) * ld + col;
+        // chunk order fixed (deterministic); loads issued four at a time
+        float acc = 0.f;
+        int ch = 0;
+        for (; ch + 4 <= a.chunks; ch += 4) {
+            const float v0 = s[ch * st], v1 = s[(ch + 1) * st], v2 = s[(ch + 2) * st], v3 = s[(ch + 3) * st];
+            acc = (((acc + v0) + v1) + v2) + v3;
+        }
+        for (; ch < a.chunks; ++ch) acc += s[ch * st];
+        a.g[dst] = acc * a.inv_gscale;
     }
-    if (job < 0) return;
-    const int ld = a.job_KB[job] * 32 + 1;
-    const float* s = a.slabs + a.job_slab[job] + static_cast<int64_t>(row) * ld + col;
-    const int64_t st = a.slab_floats_per_chunk;
-    // chunk order fixed (deterministic); loads issued four at a time
-    float acc = 0.f;
-    int c = 0;
-    for (; c + 4 <= a.chunks; c += 4) {
-        const float v0 = s[c * st], v1 = s[(c + 1) * st], v2 = s[(c + 2) * st], v3 = s[(c + 3) * st];
-        acc = (((acc + v0) + v1) + v2) + v3;
-    }
-    for (; c < a.chunks; ++c) acc += s[c * st];
-    a.g[pidx] = acc * a.inv_gscale;
 }
 
 // ---------------------------------------------------------------- pack ----
@@ -3174,8 +3173,10 @@ int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M, const void* worksp
         r.job_slab[j] = p.job[j].slab_off;
         r.job_KB[j] = p.job[j].KB;
     }
-    hipLaunchKernelGGL(mlp_dw_reduce_kernel, dim3(static_cast<unsigned>(ceil_div_ll(p.param_count, 256))), dim3(256),
-                       0, s, r);
+    int max_rows = 1;
+    for (int k = 0; k < p.n_red; ++k) max_rows = p.red[k].rows > max_rows ? p.red[k].rows : max_rows;
+    hipLaunchKernelGGL(mlp_dw_reduce_kernel, dim3(static_cast<unsigned>(max_rows), static_cast<unsigned>(p.n_red)),
+                       dim3(256), 0, s, r);
     NR_LAUNCH_CHECK("nr_mlp_backward_reduce");
     return NR_OK;
 }
