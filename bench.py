@@ -189,6 +189,44 @@ def kernel_table(wcalls, prec: str, n_params: int, steps_per_key=1):
     return out, step_bytes
 
 
+def headline_roofline(tflops: float, live_ms: float, rocprof_ms, prec: str):
+    """The dominant kernel on SURVEY §8d's MFMA basis: algorithmic FLOPs per launch over
+    its launch time -- the committed rocprof average of these sources when there is one
+    (reproducible from profiles/), else the live HIP-event time."""
+    ach = tflops * live_ms / rocprof_ms if rocprof_ms else tflops
+    return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[prec], "unit": "TFLOP/s",
+            "frac": round(ach / PEAK_TFLOPS[prec], 4)}
+
+
+def rank_topology(pg, dev, step_ms_median: float, allreduce):
+    """Self-check of a data-parallel run: the process group's size, the device
+    every rank bound, each rank's median step time and its measured all-reduce times
+    (HIP events around GradAllReducer's wait), gathered to every rank."""
+    import torch.distributed as dist
+    props = torch.cuda.get_device_properties(dev)
+    mine = [float(dist.get_rank(pg)), float(dev.index), float(getattr(props, "pci_bus_id", -1)),
+            float(getattr(props, "pci_device_id", -1)), step_ms_median,
+            allreduce["span_ms"] if allreduce else -1.0, allreduce["exposed_ms"] if allreduce else -1.0]
+    t = torch.tensor(mine, device=dev if dist.get_backend(pg) == "nccl" else "cpu", dtype=torch.float64)
+    allt = [torch.empty_like(t) for _ in range(dist.get_world_size(pg))]
+    dist.all_gather(allt, t, group=pg)
+    ranks = []
+    for v in (x.tolist() for x in allt):
+        r = {"rank": int(v[0]), "device": int(v[1]), "pci_bus_id": int(v[2]), "pci_device_id": int(v[3]),
+             "step_ms_median": round(v[4], 4)}
+        if v[5] >= 0:
+            r["allreduce_span_ms"] = round(v[5], 4)
+            r["allreduce_exposed_ms"] = round(v[6], 4)
+        ranks.append(r)
+    return {"backend": dist.get_backend(pg), "world_size": dist.get_world_size(pg),
+            "distinct_devices": len({(r["pci_bus_id"], r["pci_device_id"], r["device"]) for r in ranks}),
+            "allreduce_steps": allreduce["steps"] if allreduce else 0,
+            "allreduce_note": "HIP events on the compute stream: span = first gradient all-reduce launched "
+                              "(fine net, during the coarse backward) -> all reduced; exposed = the step's wait "
+                              "for it in GradAllReducer.finish" if allreduce else "graph replay: not timed",
+            "ranks": ranks}
+
+
 def lego_rays(n_rays: int, seed: int, device, size: int = 800):
     """Rays of the lego training cameras at size x size (focal from camera_angle_x,
     data.py:147-150)."""
@@ -570,6 +608,9 @@ def main():
             step(k)
     timer = _hip.CallTimer(mlp_entries, keys=[dom_key] if dom_key else None)
     _hip.set_timer(timer)
+    reducer = getattr(trainer, "reducer", None)
+    if reducer is not None and not args.graph:
+        reducer.timing = []  # HIP events around every step's all-reduce wait (eager steps)
     if pg is not None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -594,6 +635,11 @@ def main():
 
     per_step = sorted(a.elapsed_time(b) for a, b in zip(evs, evs[1:]))
     step_pcts = [round(per_step[min(len(per_step) - 1, int(q * len(per_step)))], 4) for q in (0.1, 0.5, 0.9)]
+    topology = None
+    if pg is not None:
+        topology = rank_topology(pg, dev, step_pcts[1], reducer.timing_summary() if reducer is not None else None)
+        if reducer is not None:
+            reducer.timing = None
     calls = timer.summary() if not args.graph else {dom_key: wcalls[dom_key]}
     if dom_key is None:
         wcalls = calls
@@ -605,6 +651,9 @@ def main():
     n_params = mf.flat_params().numel()
     bound, achieved, peak, unit, work = roofline_of(entry, M, ms, args.precision, n_params, dom_traffic)
     mf_tf, _, mf_work = mfma_roofline(entry, M, ms, args.precision)
+    if not mfma_macs_of(entry):
+        # a dominant launch without MFMA work (e.g. the slab reduction): its byte roofline
+        mf_tf, mf_work = None, work
     # the committed rocprofv3 kernel trace of this tree (same bench command): its average
     # for the dominant kernel, and the fraction it gives (the live one is `frac`)
     rp_rows, rp_src = rocprof_summary(args.precision)
@@ -641,15 +690,13 @@ def main():
         # headline: the dominant kernel on SURVEY §8d's MFMA basis (algorithmic FLOPs per
         # launch over its launch time); the stored-activation HBM view rides beside it
         "roofline": {
-            "bound": "mfma",
-            "kernel": f"{kern[0]} via {entry} (M={M} samples, fine net)",
-            "achieved": round(mf_tf * ms / rp_ms if rp_ms else mf_tf, 2),
-            "peak": PEAK_TFLOPS[args.precision],
-            "unit": "TFLOP/s",
             # frac: from the committed rocprof kernel-trace average of these sources when
-            # one exists (reproducible from profiles/), else from the live launch time
-            "frac": round((mf_tf * ms / rp_ms if rp_ms else mf_tf) / PEAK_TFLOPS[args.precision], 4),
-            "frac_mfma": round((mf_tf * ms / rp_ms if rp_ms else mf_tf) / PEAK_TFLOPS[args.precision], 4),
+            # one exists (reproducible from profiles/), else from the live launch time;
+            # MFMA basis, or the byte basis for a launch without MFMA work
+            **(headline_roofline(mf_tf, ms, rp_ms, args.precision) if mf_tf is not None else {
+                "bound": bound, "achieved": round(achieved * ms / rp_ms if rp_ms else achieved, 2), "peak": peak,
+                "unit": unit, "frac": round((achieved * ms / rp_ms if rp_ms else achieved) / peak, 4)}),
+            "kernel": f"{kern[0]} via {entry} (M={M} samples, fine net)",
             "frac_basis": (f"rocprof_ms: timed-region average of {rp_src} (same source_hash)" if rp_ms
                            else "launch_ms: HIP events on the launching stream over the eager warm-up steps "
                            "(a graph replay runs no Python)" if args.graph
@@ -658,7 +705,7 @@ def main():
             "work_per_launch": mf_work,
             "launch_ms": round(ms, 4),
             "launches": n_launch,
-            "frac_live": round(mf_tf / PEAK_TFLOPS[args.precision], 4),
+            "frac_live": round(mf_tf / PEAK_TFLOPS[args.precision], 4) if mf_tf is not None else None,
             "rocprof_ms": round(rp_ms, 4) if rp_ms else None,
             "rocprof_source": rp_src if rp_ms else None,
             "source_hash": source_hash(),
@@ -686,6 +733,8 @@ def main():
         # metric is the recorded equal-iteration comparison on the analytic scene
         "psnr": psnr_record(),
     }
+    if topology is not None:
+        out["topology"] = topology
     if rank == 0 and world == 1:
         out["batch_assembly_ms_per_step"] = batch_assembly_ms(dev, B)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.pose_opt:

@@ -210,7 +210,8 @@ int nr_mlp_forward(const NrMlpConfig* cfg, const void* packed,
 
 /* Backward: g_rgb (M,3), g_sigma (M) -> g_params (flat, OVERWRITTEN),
  * g_x (M,3) / g_d (M,3) nullable (OVERWRITTEN).  Needs the forward's
- * `saved` and rgb/sigma outputs, and nr_mlp_workspace_bytes of workspace. */
+ * `saved` and rgb/sigma outputs, and nr_mlp_workspace_bytes of workspace.
+ * Runs the split form: nr_mlp_backward_dx, _dw, _reduce.                    */
 int nr_mlp_backward(const NrMlpConfig* cfg, const void* packed,
                     const float* params, const float* x, const float* d,
                     int64_t M, const float* rgb, const float* sigma,
@@ -249,7 +250,10 @@ int nr_mlp_backward_dxdw(const NrMlpConfig* cfg, const void* packed,
  * current device, else 0.                                                   */
 int nr_mlp_backward_pipelined(const NrMlpConfig* cfg, int64_t M);
 /* Byte offset in the workspace of the pipelined backward's status word (0 = ok,
- * nonzero = a bounded wait timed out and the gradients are invalid), or -1. */
+ * nonzero = a bounded wait timed out), or -1.  A stage that finds the word set
+ * when it ends writes NaN into its dW slabs, so nr_mlp_backward_reduce then
+ * yields NaN gradients (a loud failure: the clip norm and every Adam update
+ * turn NaN) instead of silently wrong ones.                                   */
 int64_t nr_mlp_pipe_status_offset(const NrMlpConfig* cfg, int64_t M);
 
 /* ---- A13: optimizer tail  (noisy_src/train.py:112-117, train_pose_opt.py:398-409)

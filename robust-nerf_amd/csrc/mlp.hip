@@ -2671,22 +2671,25 @@ bool pipe_resident_one_per_cu() {
     return ok == 1;
 }
 
+// One compiled instance per (XB, DB, NX): the reference's encodings (pos_freqs 10:
+// XB 2), with / without view dirs and skip; other encodings run the split backward.
+// LAUNCH false: only report whether the instance exists and is resident one per CU
+// (nr_mlp_backward_pipelined), true: launch it.
 template <int PREC>
-int launch_pipe(const MlpPlan& p, const PipeArgs& a, int NX, hipStream_t s, bool* launched) {
+int launch_pipe(const MlpPlan& p, const PipeArgs& a, int NX, hipStream_t s, bool* launched, bool launch = true) {
     *launched = false;
     const dim3 grid(static_cast<unsigned>(a.npipe * a.nstage)), block(kPipeThreads);
 #define NR_PIPE(XB_, DB_, NX_)                                                                               \
     if (p.XB == XB_ && p.DB == DB_ && NX == NX_) {                                                           \
         if (!pipe_resident_one_per_cu<PREC, XB_, DB_, NX_>()) return NR_OK;                                  \
+        *launched = true;                                                                                    \
+        if (!launch) return NR_OK;                                                                           \
         hipLaunchKernelGGL((mlp_bwd_pipe_kernel<PREC, XB_, DB_, NX_>), grid, block, pipe_lds_bytes(XB_, DB_, NX_), \
                            s, a);                                                                            \
-        *launched = true;                                                                                    \
         return check_launch("nr_mlp_backward_dxdw");                                                         \
     }
     NR_PIPE(2, 1, 2)
 #ifndef NR_MLP_DEV
-    // the reference's encodings (pos_freqs 10: XB 2), with / without view dirs and skip;
-    // other encodings run the split backward
     NR_PIPE(2, 1, 1)
     NR_PIPE(2, 0, 2)
     NR_PIPE(2, 0, 1)
@@ -3258,10 +3261,19 @@ int nr_mlp_backward_pipelined(const NrMlpConfig* cfg, int64_t M) {
     if (!plan_or_error(cfg, &p) || M <= 0) return 0;
     const MlpSizes z = make_sizes(p, M);
     PipeArgs a;
+    std::memset(&a, 0, sizeof(a));
     int NX = 0;
     if (!pipe_layout(p, z, a, NX)) return 0;
+    a.npipe = z.chunks;
     const int cus = device_cus();
-    return cus > 0 && z.chunks * (p.n_layers + 2) <= cus && M <= kPipeMaxM ? 1 : 0;
+    if (!(cus > 0 && a.npipe * a.nstage <= cus && M <= kPipeMaxM)) return 0;
+    // the same instance and residency checks nr_mlp_backward_dxdw makes before it launches
+    bool ok = false;
+    if (p.prec == NR_PREC_BF16)
+        launch_pipe<NR_PREC_BF16>(p, a, NX, nullptr, &ok, false);
+    else
+        launch_pipe<NR_PREC_FP16>(p, a, NX, nullptr, &ok, false);
+    return ok ? 1 : 0;
 }
 
 int64_t nr_mlp_pipe_status_offset(const NrMlpConfig* cfg, int64_t M) {
@@ -3276,8 +3288,12 @@ int nr_mlp_backward(const NrMlpConfig* cfg, const void* packed, const float* par
                     const float* g_sigma, float* g_params, float* g_x, float* g_d, void* workspace,
                     nr_stream_t stream) {
     NR_REQUIRE(g_params, "nr_mlp_backward: null g_params");
-    int rc = nr_mlp_backward_dxdw(cfg, packed, params, x, d, M, rgb, sigma, saved, g_rgb, g_sigma, g_x, g_d,
-                                  workspace, stream);
+    // the split form (dX chain, dW GEMM), as noisy_src's default; nr_mlp_backward_dxdw is
+    // the layer-pipelined alternative for callers that choose it
+    int rc = nr_mlp_backward_dx(cfg, packed, params, x, d, M, rgb, sigma, saved, g_rgb, g_sigma, g_x, g_d, workspace,
+                                stream);
+    if (rc) return rc;
+    rc = nr_mlp_backward_dw(cfg, M, saved, workspace, stream);
     if (rc) return rc;
     return nr_mlp_backward_reduce(cfg, M, workspace, g_params, stream);
 }

@@ -152,7 +152,10 @@ struct MlpSizes {
 };
 
 // ring slots per edge and 32-bit flag words per (pipeline, edge) of the fused backward
-constexpr int kPipeRingSlots = 32;
+#ifndef NR_PIPE_RING
+#define NR_PIPE_RING 32
+#endif
+constexpr int kPipeRingSlots = NR_PIPE_RING;
 constexpr int kPipeFlagWordsPerEdge = 128;
 #ifdef NR_PIPE_PROF
 constexpr int kPipeStatusWordsHead = 64 + 512 * 32;  // + per-workgroup timing records (diagnostic builds)

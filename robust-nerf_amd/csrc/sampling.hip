@@ -7,11 +7,20 @@
 // order, as torch's CPU cumsum); u = linspace(0,1,Ns) if det else the caller's
 // uniforms; idx = searchsorted(cdf, u, right=True); below/above clamped; the
 // `denom < 1e-5 -> 1` rule; s = b0 + (u-c0)/denom * (b1-b0).  The hierarchical
-// form then sorts cat(z_coarse, s) — here an all-pairs rank sort in LDS, whose
+// form then sorts cat(z_coarse, s) — here a bitonic sort in the wave's LDS, whose
 // output values equal torch.sort's whatever the order of u.
 #include "common.hpp"
 
 namespace nr {
+
+// Lanes of one wave exchanging values through LDS: the wave barrier alone is not a
+// memory fence at the IR level, so release / acquire at wavefront scope around it keep
+// the compiler from moving or forwarding LDS accesses across it (rocPRIM's wave sync).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 constexpr int kRaysPerBlock = 4;  // one wave per ray
 constexpr int kMaxPerLane = 8;    // Nc + Nf <= 512
@@ -36,13 +45,13 @@ __device__ __forceinline__ void build_cdf(float* wbuf, float* cdf, int nb, int l
         const int k = lane + 64 * j;
         pdf[j] = k < nw ? (wbuf[k] + 1e-5f) / sum : 0.f;
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int k = lane + 64 * j;
         if (k < nw) wbuf[k] = pdf[j];
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     float run = 0.f;
     if (lane == 0) cdf[0] = 0.f;
     for (int k = 0; k < nw; ++k) {
@@ -131,7 +140,7 @@ __global__ void sample_hier_kernel(const float* ro, const float* rd, const float
     // equal values cannot show).  An all-pairs rank sort cost T^2 compares per ray.
     const int P = P2;
     for (int e = T + lane; e < P; e += 64) uni[e] = __builtin_inff();
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     for (int k = 2; k <= P; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int t = lane; t < (P >> 1); t += 64) {
@@ -143,7 +152,7 @@ __global__ void sample_hier_kernel(const float* ro, const float* rd, const float
                     uni[hi] = x;
                 }
             }
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_sync();
         }
     }
     const int64_t ob = static_cast<int64_t>(b) * T;

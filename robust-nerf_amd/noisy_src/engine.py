@@ -134,6 +134,11 @@ class GradAllReducer:
         self.world = dist.get_world_size(process_group)
         self.average = average
         self.pending = []
+        # timing (bench.py): per eager step, HIP events on the compute stream at the first
+        # launch, before ``finish`` waits and after it: (launch -> done) is the collective's
+        # span beside the rest of the backward, (wait -> done) what the step is exposed to
+        self.timing = None
+        self._t_launch = None
 
     @property
     def prescale(self) -> float:
@@ -147,16 +152,38 @@ class GradAllReducer:
             self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group)
             self.pending.append((None, flat))
             return
+        if self.timing is not None and flat.is_cuda and not self.pending:
+            self._t_launch = torch.cuda.Event(enable_timing=True)
+            self._t_launch.record()
         work = self.dist.all_reduce(flat, op=self.dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.pending.append((work, flat))
 
     def finish(self) -> None:
+        timed = self.timing is not None and self._t_launch is not None
+        if timed:
+            t_wait = torch.cuda.Event(enable_timing=True)
+            t_wait.record()
         for work, flat in self.pending:
             if work is not None:
                 work.wait()
             if self.average and self.world > 1:
                 flat.mul_(1.0 / self.world)
+        if timed:
+            t_done = torch.cuda.Event(enable_timing=True)
+            t_done.record()
+            self.timing.append((self._t_launch, t_wait, t_done))
+        self._t_launch = None
         self.pending.clear()
+
+    def timing_summary(self) -> Optional[Dict[str, float]]:
+        """Means over the recorded steps (ms): ``span`` = first launch -> all reduced,
+        ``exposed`` = the compute stream's wait in ``finish``; None without records."""
+        if not self.timing:
+            return None
+        torch.cuda.synchronize()
+        span = [a.elapsed_time(c) for a, _, c in self.timing]
+        exposed = [b.elapsed_time(c) for _, b, c in self.timing]
+        return {"steps": len(span), "span_ms": sum(span) / len(span), "exposed_ms": sum(exposed) / len(exposed)}
 
 
 class Trainer:

@@ -190,8 +190,9 @@ def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
           process_group=None, log=print, graph: bool = False) -> Dict[str, object]:
     """Reference train.py:307-577.  ``train_data`` / ``val_data`` (optional) replace the
     on-disk scene; ``process_group`` (or a torchrun environment, see ``main``) makes it
-    data parallel.  ``graph`` (one process only) replays the training step from a hipGraph
-    after the first iteration (``engine.GraphedTrainer``; same results as eager).
+    data parallel.  ``graph`` replays the training step from a hipGraph after the first
+    iteration (``engine.GraphedTrainer``; same results as eager); with data parallelism
+    the RCCL all-reduces are captured into it too (``nccl`` backend only).
     Returns the networks, the output directory and the final metrics."""
     import torch.distributed as dist
 
@@ -361,7 +362,8 @@ def build_arg_parser():
     ap.add_argument("--precision", type=str, default="fp32", choices=["fp32", "bf16", "fp16"],
                     help="MLP operand precision (fp32 = the reference's numerics)")
     ap.add_argument("--graph", action="store_true",
-                    help="replay the training step from a hipGraph (one process; same results as eager)")
+                    help="replay the training step from a hipGraph (same results as eager; with RCCL data "
+                         "parallelism the all-reduces are captured too)")
     return ap
 
 

@@ -23,10 +23,12 @@ def bench(prec, M, reps=int(__import__("os").environ.get("MB_REPS", "20"))):
         "fwd_train": lambda: _hip.call("nr_mlp_forward", cfg, P(packed), P(flat), P(x), P(d), M, P(rgb), P(sig), P(saved), st),
         "bwd_dx": lambda: _hip.call("nr_mlp_backward_dx", cfg, P(packed), P(flat), P(x), P(d), M, P(rgb), P(sig), P(saved), P(grgb), P(gs), None, None, P(ws), st),
         "bwd_dw": lambda: _hip.call("nr_mlp_backward_dw", cfg, M, P(saved), P(ws), st),
+        "bwd_dxdw": lambda: _hip.call("nr_mlp_backward_dxdw", cfg, P(packed), P(flat), P(x), P(d), M, P(rgb), P(sig), P(saved), P(grgb), P(gs), None, None, P(ws), st),
         "bwd_reduce": lambda: _hip.call("nr_mlp_backward_reduce", cfg, M, P(ws), P(gflat), st),
     }
     out = {}
-    for name in ("fwd_infer", "fwd_train", "bwd_dx", "bwd_dw", "bwd_reduce"):
+    names = __import__("os").environ.get("MB_KERNELS", "fwd_infer,fwd_train,bwd_dx,bwd_dw,bwd_dxdw,bwd_reduce")
+    for name in names.split(","):
         fn = fns[name]
         fn(); torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

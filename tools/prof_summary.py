@@ -36,7 +36,11 @@ FAMILIES = {"mlp_fwd_kernel": "nr_mlp_forward", "mlp_bwd_kernel": "nr_mlp_backwa
 
 def source_hash() -> str:
     """sha1 over the HIP sources and the ABI header (bench.py computes the same hash, so
-    it uses a kernel summary only when it was profiled from the benchmarked sources)."""
+    it uses a kernel summary only when it was profiled from the benchmarked sources);
+    NR_SOURCE_HASH overrides it when re-summarising a trace taken from an older tree."""
+    import os
+    if os.environ.get("NR_SOURCE_HASH"):
+        return os.environ["NR_SOURCE_HASH"]
     h = hashlib.sha1()
     files = sorted((ROOT / "robust-nerf_amd" / "csrc").glob("*")) + [ROOT / "include" / "nerf_hip.h"]
     for f in files:
@@ -56,15 +60,39 @@ def precision_of(name: str) -> str:
     return {"1": "bf16", "0": "fp32", "2": "fp16"}.get(m.group(1), "") if m else ""
 
 
-def sample_count(name: str, grid: int, last_M: int) -> int:
-    """M of a fused-MLP launch: the forward/backward kernels run one 32-sample tile per
-    wave; dW and its reduction follow the backward launch of the same M in the stream."""
-    fam = short(name)
-    if fam in ("mlp_fwd_kernel", "mlp_bwd_kernel", "mlp_fwd_rbm_kernel", "mlp_bwd_rbm_kernel"):
-        return grid // 64 * 32
-    if fam in ("mlp_dw_kernel", "mlp_dw_reduce_kernel", "mlp_dinput_kernel", "mlp_bwd_pipe_kernel"):
-        return last_M
-    return 0
+def is_training_forward(name: str) -> bool:
+    """A forward launch that saves activations (TRAIN template flag) and so has exactly
+    one backward launch later in the step."""
+    return short(name) in ("mlp_fwd_kernel", "mlp_fwd_rbm_kernel") and "true" in name.split("(")[0]
+
+
+class MTracker:
+    """M of every fused-MLP launch in stream order.  The forward / dX kernels run one
+    32-sample tile per wave, so their grid gives M.  dW, its reduction and the input
+    gradients follow the backward launch of the same M.  The fused layer-pipelined
+    backward's grid is pipelines x stages (independent of M): it belongs to the training
+    forward of the same net, and autograd runs the backwards in reverse forward order
+    (fine before coarse), so each one pops the newest unmatched training forward."""
+
+    def __init__(self):
+        self.last = 0
+        self.fwd_stack = []
+
+    def __call__(self, name: str, grid: int) -> int:
+        fam = short(name)
+        M = 0
+        if fam in ("mlp_fwd_kernel", "mlp_bwd_kernel", "mlp_fwd_rbm_kernel", "mlp_bwd_rbm_kernel"):
+            M = grid // 64 * 32
+            if is_training_forward(name):
+                self.fwd_stack.append(M)
+            elif fam in ("mlp_bwd_kernel", "mlp_bwd_rbm_kernel") and self.fwd_stack:
+                self.fwd_stack.pop()
+        elif fam == "mlp_bwd_pipe_kernel":
+            M = self.fwd_stack.pop() if self.fwd_stack else self.last
+        elif fam in ("mlp_dw_kernel", "mlp_dw_reduce_kernel", "mlp_dinput_kernel"):
+            M = self.last
+        self.last = M or self.last
+        return M
 
 
 def main(out_dir: str, tag: str, timed_steps: int = 0) -> None:
@@ -74,11 +102,10 @@ def main(out_dir: str, tag: str, timed_steps: int = 0) -> None:
     rows = defaultdict(list)
     with open(base / "prof" / "run_kernel_trace.csv") as f:
         trace = sorted(csv.DictReader(f), key=lambda r: int(r["Dispatch_Id"]))
-    last_M = 0
+    track = MTracker()
     for r in trace:
         grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
-        M = sample_count(r["Kernel_Name"], grid, last_M)
-        last_M = M or last_M
+        M = track(r["Kernel_Name"], grid)
         rows[(r["Kernel_Name"], grid, M)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     summ = ROOT / "profiles" / f"{tag}_kernel_summary.csv"
     with open(summ, "w", newline="") as f:
@@ -101,10 +128,9 @@ def main(out_dir: str, tag: str, timed_steps: int = 0) -> None:
         with open(p) as f:
             recs_ = sorted((r for r in csv.DictReader(f) if r["Counter_Name"] == cname),
                            key=lambda r: int(r["Dispatch_Id"]))
-        last_M = 0
+        track = MTracker()
         for r in recs_:
-            M = sample_count(r["Kernel_Name"], int(r["Grid_Size"]), last_M)
-            last_M = M or last_M
+            M = track(r["Kernel_Name"], int(r["Grid_Size"]))
             key = (r["Kernel_Name"], M)
             counters[key][cname].append(float(r["Counter_Value"]) * 1024.0)  # KB -> B
     recs = []
@@ -117,6 +143,9 @@ def main(out_dir: str, tag: str, timed_steps: int = 0) -> None:
         recs.append({"kernel": fam, "entry": FAMILIES[fam], "precision": precision_of(k), "M": M,
                      "fetch_size_bytes": fetch, "write_size_bytes": write,
                      "bytes_per_launch": 2.0 * fetch + write, "launches": len(c["FETCH_SIZE"])})
+    if not recs:
+        print("no PMC passes under", base, "- profiles/traffic.json left as it is")
+        return
     out = {"source_hash": source_hash(),
            "source": f"profiles/{tag}: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
                      "python bench.py --steps 2 --warmup 1 --no-cpu-baseline; traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (median)",
