@@ -36,7 +36,9 @@
 #if defined(NR_NOSTORE_IMG) || defined(NR_RBM_NOWAIT) || (defined(NR_DW_NOCOMPUTE) && NR_DW_NOCOMPUTE) || \
     (defined(NR_DW_NOBIAS) && NR_DW_NOBIAS) || (defined(NR_AB_NODMA) && NR_AB_NODMA) ||                   \
     (defined(NR_AB_NOBAR) && NR_AB_NOBAR) || (defined(NR_AB_NOWAIT) && NR_AB_NOWAIT) ||                   \
-    (defined(NR_AB_HALFA) && NR_AB_HALFA) || (defined(NR_FWD_NOSINK) && NR_FWD_NOSINK)
+    (defined(NR_AB_HALFA) && NR_AB_HALFA) || (defined(NR_FWD_NOSINK) && NR_FWD_NOSINK) || defined(NR_PIPE_ONLY) || \
+    (defined(NR_AB_PIPE_NORING) && NR_AB_PIPE_NORING) || (defined(NR_AB_PIPE_NOSTAGE) && NR_AB_PIPE_NOSTAGE) || \
+    (defined(NR_AB_PIPE_NOWAIT) && NR_AB_PIPE_NOWAIT)
 #error "wrong-result A/B switch in a product build: build it with tools/build_variant.sh (NR_AB_VARIANT)"
 #endif
 #endif
@@ -2581,6 +2583,10 @@ bool pipe_layout(const MlpPlan& p, const MlpSizes& z, PipeArgs& a, int& NX) {
         xl[x] = xj.dz[x].tensor - WS_DZ0;
     }
     if (xl[0] != 0 || (NX == 2 && (xl[1] < 1 || xl[1] >= n))) return false;
+    // S_X reads the skip layer's dz and dz_0, which the chain of trunk stages delivers ~4
+    // tiles per hop later (mlp_pipe.inc, the schedule): the skip layer's producer runs that
+    // far ahead of S_X's frees, so its ring must hold the lag
+    if (NX == 2 && 4 * xl[1] + 8 > kPipeRingSlots) return false;
     for (int i = 1; i < n; ++i) {
         const DwJob& j = p.job[i];
         if (j.ndz != 1 || j.nin != 1 || !j.dz[0].is_ws || j.dz[0].tensor != WS_DZ0 + i || j.in[0].is_ws ||

@@ -19,8 +19,10 @@ from noisy_src._hip import call, ptr  # noqa: E402
 from noisy_src.config import ModelConfig  # noqa: E402
 from noisy_src.model import NeRF  # noqa: E402
 
-SEG = {2: "top-wait", 3: "bar+sig", 4: "free-wait", 5: "dX+st", 6: "S6wait/spin", 7: "poll+stage", 8: "dW",
-       9: "bar+dma", 10: "heads"}
+# segments of the v2 stage loops (csrc/mlp_pipe.inc, pf.seg(i)): trunk/feat 2 3 4 5 6 7,
+# dir 2 10 3 4 5 7 8, x 2 3 4 6 7
+SEG = {2: "top-wait", 3: "bar+sig", 4: "store+rdy", 5: "dX", 6: "poll+ld", 7: "dW|poll+ld", 8: "dW",
+       9: "-", 10: "heads"}
 KIND = {0: "dir", 1: "feat", 2: "trunk", 3: "x"}
 
 
