@@ -482,6 +482,9 @@ def main():
                          "data parallelism the RCCL all-reduces are captured too)")
     ap.add_argument("--dp", action="store_true",
                     help="join an RCCL process group even at N=1 (the data-parallel step, all-reduce hooks active)")
+    ap.add_argument("--coarse-stream", action="store_true",
+                    help="run the coarse network's chain on a second stream beside the fine one "
+                         "(engine.Trainer(coarse_stream=True); with --graph: two branches of the graph)")
     ap.add_argument("--pose-opt", action="store_true",
                     help="BASELINE cfg #3: joint pose optimisation step (train_pose_opt, poses optimising)")
     args = ap.parse_args()
@@ -562,7 +565,7 @@ def main():
             gen = torch.Generator(device=dev).manual_seed(1000 * rank)
             pool = [sampler.sample_batch(generator=gen) for _ in range(4)]
     else:
-        trainer = Trainer(mc, mf, rcfg, process_group=pg)
+        trainer = Trainer(mc, mf, rcfg, process_group=pg, coarse_stream=args.coarse_stream)
         if strong:
             pool = [tuple(x[sl] for x in lego_rays(args.global_batch, 1000 + k, dev)) for k in range(4)]
         else:
@@ -686,6 +689,7 @@ def main():
             "parallelism": f"dp{world}" + (" (RCCL process group, all-reduce in the step)" if pg is not None
                                            and world == 1 else ""),
             **({"execution": "hipGraph replay (engine.GraphedTrainer)"} if args.graph else {}),
+            **({"coarse_stream": "coarse chain on a second stream"} if args.coarse_stream else {}),
         },
         # headline: the dominant kernel on SURVEY §8d's MFMA basis (algorithmic FLOPs per
         # launch over its launch time); the stored-activation HBM view rides beside it

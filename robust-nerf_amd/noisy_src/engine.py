@@ -187,8 +187,17 @@ class GradAllReducer:
 
 
 class Trainer:
+    """One reference training iteration (train.py:68-119) on the HIP kernels.
+    ``coarse_stream``: run the coarse network's forward, compositing and (through
+    autograd's stream semantics) their backward on a second stream beside the fine
+    network's; bit-identical to the one-stream step.  It pays where one chain does not
+    fill the GPU (BASELINE cfg #4's 512 rays per rank; inside a GraphedTrainer capture the
+    two chains become two branches of the graph)."""
+
     def __init__(self, model_coarse, model_fine, render_config, lr: float = 5e-4, lr_decay: int = 250,
-                 max_norm: float = 1.0, process_group=None):
+                 max_norm: float = 1.0, process_group=None, coarse_stream: bool = False):
+        self.coarse_stream = coarse_stream
+        self._cstream = None
         self.model_coarse = model_coarse
         self.model_fine = model_fine
         self.render_config = render_config
@@ -210,8 +219,13 @@ class Trainer:
     def step(self, rays_o: torch.Tensor, rays_d: torch.Tensor, target_rgb: torch.Tensor,
              t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         self.optimizer.zero_grad(set_to_none=True)
+        cs = None
+        if self.coarse_stream and self.model_fine is not None and rays_o.is_cuda:
+            if self._cstream is None or self._cstream.device != rays_o.device:
+                self._cstream = torch.cuda.Stream(device=rays_o.device)
+            cs = self._cstream
         out = render_rays(self.model_coarse, self.model_fine, rays_o, rays_d, self.render_config, is_train=True,
-                          t_rand=t_rand, u=u)
+                          t_rand=t_rand, u=u, coarse_stream=cs)
         gs = self.reducer.prescale if self.reducer is not None else 1.0  # DP: 1/world in the seed
         loss_c = ops.mse_loss(out["rgb_coarse"], target_rgb, gs)
         loss = loss_c
@@ -221,6 +235,8 @@ class Trainer:
             loss = loss_c + loss_f
             metrics["loss_fine"] = loss_f.detach()
         loss.backward(ops.unit_grad(loss.device))
+        if cs is not None:
+            torch.cuda.current_stream(rays_o.device).wait_stream(cs)  # join the coarse chain's backward
         if self.reducer is not None:
             flats = [flat for _, flat in self.reducer.pending]
             self.reducer.finish()

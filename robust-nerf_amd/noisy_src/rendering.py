@@ -42,9 +42,17 @@ def raw2outputs(rgb: torch.Tensor, sigma: torch.Tensor, z_vals: torch.Tensor, ra
 
 def render_rays(model_coarse: NeRF, model_fine: Optional[NeRF], rays_o: torch.Tensor, rays_d: torch.Tensor,
                 config: RenderConfig, is_train: bool = True, t_rand: Optional[torch.Tensor] = None,
-                u: Optional[torch.Tensor] = None, return_aux: bool = False) -> Dict[str, torch.Tensor]:
+                u: Optional[torch.Tensor] = None, return_aux: bool = False,
+                coarse_stream: Optional[torch.cuda.Stream] = None) -> Dict[str, torch.Tensor]:
     """Reference rendering.py:119-240.  ``t_rand`` / ``u`` inject the jitter and
-    inverse-CDF uniforms (otherwise drawn with torch.rand as the reference does)."""
+    inverse-CDF uniforms (otherwise drawn with torch.rand as the reference does).
+
+    ``coarse_stream``: the coarse network's forward and compositing run on that stream
+    (forked from and joined back into the current one), so autograd runs their backward
+    there too, beside the fine network's (the two chains are independent: the fine
+    samples depend on the coarse weights only through detached z values, reference
+    rays.py:325).  Same kernels, same results; the caller joins the stream after
+    ``backward``."""
     perturb = config.perturb if is_train else False
     raw_noise_std = config.raw_noise_std if is_train else 0.0
     N_rays = rays_o.shape[0]
@@ -54,9 +62,18 @@ def render_rays(model_coarse: NeRF, model_fine: Optional[NeRF], rays_o: torch.Te
     pts, z_c = ops.stratified_sample(rays_o, rays_d, config.near, config.far, Nc,
                                      t_rand=t_rand if perturb else None)
     vd = ops.expand_viewdirs(rays_d, Nc)
-    rgb_c, sigma_c = model_coarse(pts.reshape(-1, 3), vd)
-    out_c = raw2outputs(rgb_c.reshape(N_rays, Nc, 3), sigma_c.reshape(N_rays, Nc, 1), z_c, rays_d,
-                        raw_noise_std=raw_noise_std, white_background=config.white_background)
+    if coarse_stream is not None:
+        main = torch.cuda.current_stream(rays_o.device)
+        coarse_stream.wait_stream(main)
+        with torch.cuda.stream(coarse_stream):
+            rgb_c, sigma_c = model_coarse(pts.reshape(-1, 3), vd)
+            out_c = raw2outputs(rgb_c.reshape(N_rays, Nc, 3), sigma_c.reshape(N_rays, Nc, 1), z_c, rays_d,
+                                raw_noise_std=raw_noise_std, white_background=config.white_background)
+        main.wait_stream(coarse_stream)
+    else:
+        rgb_c, sigma_c = model_coarse(pts.reshape(-1, 3), vd)
+        out_c = raw2outputs(rgb_c.reshape(N_rays, Nc, 3), sigma_c.reshape(N_rays, Nc, 1), z_c, rays_d,
+                            raw_noise_std=raw_noise_std, white_background=config.white_background)
     results = {
         "rgb_coarse": out_c["rgb_map"],
         "depth_coarse": out_c["depth_map"],
