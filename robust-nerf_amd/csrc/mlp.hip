@@ -210,9 +210,6 @@ __device__ __forceinline__ void pe_feat_bwd(float x0, float x1, float x2, int f,
 #ifndef NR_AB_NOBAR
 #define NR_AB_NOBAR 0  // A/B timing only (racy): no stream barrier
 #endif
-#ifndef NR_DW_CHUNK_MAJOR
-#define NR_DW_CHUNK_MAJOR 1
-#endif
 #ifndef NR_NT_STORE
 #define NR_NT_STORE 1
 #endif
@@ -1682,17 +1679,19 @@ constexpr int kDwThreads = 512;
 constexpr int kDwWaves = kDwThreads / 64;
 static_assert(kDwWaves == kDwMaxWaves, "dW wave shares are planned for 8-wave workgroups");
 
+constexpr int kDwMaxWgs = 256;  // one round of workgroups (make_sizes: NR_DW_WGS)
 struct DwArgs {
     float* slabs;
     int njobs;
     int64_t tiles;
-    int tiles_per_chunk, chunks;
+    int job_tpc[kMaxJobs];          // tiles per chunk of each job
+    uint16_t wg_map[kDwMaxWgs];     // workgroup -> job | chunk << 5 (chunk-major: one chunk of every job in a row)
     int stage_bytes, nstage;
     int64_t slab_floats_per_chunk;
     int job_NBz[kMaxJobs], job_KB[kMaxJobs], job_nseg[kMaxJobs];
     int64_t job_slab[kMaxJobs];
     const char* seg_ptr[kMaxJobs][2 * kMaxJobSeg];  // tensor region: dz segments, then inputs
-    int seg_blocks[kMaxJobs][2 * kMaxJobSeg];  // int: scalar-loadable
+    uint8_t seg_blocks[kMaxJobs][2 * kMaxJobSeg];
     // wave share (DwWave) packed: row0 | np << 6 | col0 << 9 | nq << 15 | bias << 17; 0 = idle
     int job_wave[kMaxJobs][kDwWaves];
 };
@@ -1773,20 +1772,17 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar staging loop
-#if NR_DW_CHUNK_MAJOR
-    // chunk-major: every job of a chunk runs at about the same time (an input two
+    // chunk-major (wg_map): every job of a chunk runs at about the same time (an input two
     // jobs share, x_enc of the x-jobs beyond the first, is re-read from L2/MALL)
-    const int j = blockIdx.x % a.njobs, chunk = blockIdx.x / a.njobs;
-#else
-    const int j = blockIdx.x / a.chunks, chunk = blockIdx.x % a.chunks;
-#endif
+    const int wmap = a.wg_map[blockIdx.x];
+    const int j = wmap & 31, chunk = wmap >> 5;
     const int NBz = a.job_NBz[j], KB = a.job_KB[j];
     const int winfo = a.job_wave[j][wv];
     const int row0 = winfo & 63, np = (winfo >> 6) & 7, col0 = (winfo >> 9) & 63, nq = (winfo >> 15) & 3;
     const bool active = np > 0;
     const bool do_bias = active && ((winfo >> 17) & 1);
-    const int64_t t0 = static_cast<int64_t>(chunk) * a.tiles_per_chunk;
-    int64_t t1 = t0 + a.tiles_per_chunk;
+    const int64_t t0 = static_cast<int64_t>(chunk) * a.job_tpc[j];
+    int64_t t1 = t0 + a.job_tpc[j];
     if (t1 > a.tiles) t1 = a.tiles;
     constexpr int FPB = kFPB<PREC>;
     constexpr int BLK = FPB * kFragBytes;
@@ -2029,7 +2025,6 @@ struct ReduceArgs {
     float* g;
     float inv_gscale;  // fp16: undo the backward's loss scale (a power of two: exact)
     int64_t param_count;
-    int chunks;
     int64_t slab_floats_per_chunk;
     int n_red;
     int rows[kMaxRed], in[kMaxRed], nseg[kMaxRed], bjob[kMaxRed], brow0[kMaxRed];
@@ -2037,6 +2032,7 @@ struct ReduceArgs {
     RedSeg seg[kMaxRed][kMaxSeg];
     int64_t job_slab[kMaxJobs];
     int job_KB[kMaxJobs];
+    int job_chunks[kMaxJobs];  // slab sets of each job, summed in chunk order
 };
 
 // One workgroup per (reduce range k = blockIdx.y, output row r = blockIdx.x): the row's
@@ -2070,13 +2066,14 @@ __global__ void mlp_dw_reduce_kernel(ReduceArgs a) {
         const int ld = a.job_KB[job] * 32 + 1;
         const float* s = a.slabs + a.job_slab[job] + static_cast<int64_t>(row) * ld + col;
         // chunk order fixed (deterministic); loads issued four at a time
+        const int nch = a.job_chunks[job];
         float acc = 0.f;
         int ch = 0;
-        for (; ch + 4 <= a.chunks; ch += 4) {
+        for (; ch + 4 <= nch; ch += 4) {
             const float v0 = s[ch * st], v1 = s[(ch + 1) * st], v2 = s[(ch + 2) * st], v3 = s[(ch + 3) * st];
             acc = (((acc + v0) + v1) + v2) + v3;
         }
-        for (; ch < a.chunks; ++ch) acc += s[ch * st];
+        for (; ch < nch; ++ch) acc += s[ch * st];
         a.g[dst] = acc * a.inv_gscale;
     }
 }
@@ -3093,9 +3090,17 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
     std::memset(&w, 0, sizeof(w));
     w.slabs = reinterpret_cast<float*>(ws + z.slab_off);
     w.tiles = z.tiles;
-    w.chunks = z.chunks;
     w.njobs = p.n_jobs;
-    w.tiles_per_chunk = static_cast<int>(ceil_div_ll(z.tiles, z.chunks));
+    int nwg = 0;
+    NR_REQUIRE(p.n_jobs <= 32 && z.max_chunks < 2048, "nr_mlp_backward_dw: %d jobs x %d chunks beyond the map",
+               p.n_jobs, z.max_chunks);
+    for (int c = 0; c < z.max_chunks; ++c)
+        for (int j = 0; j < p.n_jobs; ++j)
+            if (c < z.job_chunks[j]) {
+                NR_REQUIRE(nwg < kDwMaxWgs, "nr_mlp_backward_dw: more than %d workgroups", kDwMaxWgs);
+                w.wg_map[nwg++] = static_cast<uint16_t>(j | c << 5);
+            }
+    for (int j = 0; j < p.n_jobs; ++j) w.job_tpc[j] = static_cast<int>(ceil_div_ll(z.tiles, z.job_chunks[j]));
     w.slab_floats_per_chunk = p.slab_floats_per_chunk;
     int max_blk = 0;
     for (int j = 0; j < p.n_jobs; ++j) {
@@ -3117,11 +3122,11 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
         int ns = 0;
         for (int q = 0; q < jb.ndz; ++q, ++ns) {
             w.seg_ptr[j][ns] = (jb.dz[q].is_ws ? ws : sv) + (jb.dz[q].is_ws ? z.ws_off : z.saved_off)[jb.dz[q].tensor];
-            w.seg_blocks[j][ns] = jb.dz[q].blocks;
+            w.seg_blocks[j][ns] = static_cast<uint8_t>(jb.dz[q].blocks);
         }
         for (int q = 0; q < jb.nin; ++q, ++ns) {
             w.seg_ptr[j][ns] = (jb.in[q].is_ws ? ws : sv) + (jb.in[q].is_ws ? z.ws_off : z.saved_off)[jb.in[q].tensor];
-            w.seg_blocks[j][ns] = jb.in[q].blocks;
+            w.seg_blocks[j][ns] = static_cast<uint8_t>(jb.in[q].blocks);
         }
         w.job_nseg[j] = ns;
         w.job_slab[j] = jb.slab_off;
@@ -3136,7 +3141,7 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
     const size_t lds = static_cast<size_t>(w.nstage) * w.stage_bytes + kFragBytes;
     NR_REQUIRE(w.nstage >= 2, "nr_mlp_backward_dw: a %d-byte stage does not fit twice in LDS", w.stage_bytes);
     NR_REQUIRE(lds <= 160 * 1024, "nr_mlp_backward_dw: %zu bytes of LDS staging exceeds 160 KiB", lds);
-    const dim3 grid(static_cast<unsigned>(p.n_jobs * z.chunks)), block(kDwThreads);
+    const dim3 grid(static_cast<unsigned>(nwg)), block(kDwThreads);
     if (p.prec == NR_PREC_BF16)
         hipLaunchKernelGGL(mlp_dw_kernel<NR_PREC_BF16>, grid, block, lds, s, w);
     else if (p.prec == NR_PREC_FP16)
@@ -3164,7 +3169,6 @@ int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M, const void* worksp
     r.g = g_params;
     r.inv_gscale = 1.0f / grad_scale(p.prec);
     r.param_count = p.param_count;
-    r.chunks = z.chunks;
     r.slab_floats_per_chunk = p.slab_floats_per_chunk;
     r.n_red = p.n_red;
     for (int k = 0; k < p.n_red; ++k) {
@@ -3181,6 +3185,7 @@ int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M, const void* worksp
     for (int j = 0; j < p.n_jobs; ++j) {
         r.job_slab[j] = p.job[j].slab_off;
         r.job_KB[j] = p.job[j].KB;
+        r.job_chunks[j] = z.job_chunks[j];
     }
     int max_rows = 1;
     for (int k = 0; k < p.n_red; ++k) max_rows = p.red[k].rows > max_rows ? p.red[k].rows : max_rows;

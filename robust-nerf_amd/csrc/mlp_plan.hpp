@@ -142,6 +142,8 @@ struct MlpSizes {
     int64_t saved_bytes;
     int64_t ws_off[kMaxTrunk + 3];     // bytes
     int chunks;                        // dW split over sample tiles (= pipelines of the fused backward)
+    int job_chunks[kMaxJobs];          // dW workgroups of each job (16-bit: all = chunks; fp32: by cost)
+    int max_chunks;                    // per-chunk slab sets allocated (the largest job_chunks)
     int64_t slab_off;                  // bytes
     // fused 16-bit backward (mlp_pipe.inc): status + flag words (zeroed every call), then
     // the dz rings, [pipeline][edge][slot] 16-KB tiles; edges = dz_0 .. dz_{n-1}, dz_feat

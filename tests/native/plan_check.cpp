@@ -59,5 +59,22 @@ int main(int argc, char** argv) {
         }
     }
     printf("params %ld (plan %ld) unwritten %ld doubly written %ld\n", n, (long)p.param_count, bad, dup);
-    return bad != 0 || dup != 0 || n != p.param_count;
+    // dW workgroups per job (make_sizes): one round, every job at least one chunk, the
+    // slab sets cover the largest job; uniform for 16-bit (the pipelined backward's chunks)
+    long wg_bad = 0;
+    for (long M : {1L, 5000L, 262144L, 786432L}) {
+        const MlpSizes z = make_sizes(p, M);
+        int tot = 0, mx = 0;
+        printf("M %ld chunks %d max %d:", M, z.chunks, z.max_chunks);
+        for (int j = 0; j < p.n_jobs; ++j) {
+            printf(" %d", z.job_chunks[j]);
+            tot += z.job_chunks[j];
+            mx = z.job_chunks[j] > mx ? z.job_chunks[j] : mx;
+            wg_bad += z.job_chunks[j] < 1 || (p.fpb == 2 && z.job_chunks[j] != z.chunks);
+        }
+        printf(" (sum %d)\n", tot);
+        wg_bad += tot > 256 || mx != z.max_chunks;
+    }
+    printf("dW workgroup plan bad %ld\n", wg_bad);
+    return bad != 0 || dup != 0 || n != p.param_count || wg_bad != 0;
 }

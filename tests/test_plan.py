@@ -35,6 +35,7 @@ def test_every_parameter_gradient_written_once(plan_check, cfg):
     r = subprocess.run([str(plan_check), *map(str, cfg)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "unwritten 0 doubly written 0" in r.stdout
+    assert "dW workgroup plan bad 0" in r.stdout
 
 
 def test_too_many_dw_jobs_fails_cleanly(plan_check):
