@@ -12,8 +12,10 @@ weights and see the same ray batches and the same stratified / inverse-CDF draws
 * ``hip``  — this package's engine.Trainer (HIP kernels, fused clip + Adam), fp32 or bf16.
 
 Test PSNR is the mean over the test views of -10 log10(MSE) of deterministic renders.
-``python tests/psnr_parity.py [iters] [size] [seeds] [out.json] [lr_decay]`` writes the
-record (default profiles/r02_psnr_parity.json).  ``lr_decay`` is the reference's
+``python tests/psnr_parity.py [iters] [size] [seeds] [out.json] [lr_decay] [workers]
+[first_seed]`` writes the record (default profiles/r02_psnr_parity.json); ``--merge out.json
+a.json b.json ...`` pools the runs of several records (disjoint seed ranges of one setup)
+into one paired summary.  ``lr_decay`` is the reference's
 TrainConfig.lr_decay (LambdaLR 0.1^(step / (lr_decay * 1000)), train.py:405-411): at the
 default 250 the LR is constant over a short run and the final PSNR of two runs that
 differ by one rounding keeps fluctuating chaotically by ~0.7 dB; lr_decay = 1 anneals
@@ -151,6 +153,9 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--from-log":
         from_log(sys.argv[2], Path(sys.argv[3]), note=sys.argv[4] if len(sys.argv) > 4 else None)
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "--merge":
+        merge(Path(sys.argv[2]), [Path(a) for a in sys.argv[3:]])
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "--worker":
         it, size, batch, lr_decay = (int(v) for v in sys.argv[2:6])
         worker(it, size, batch, lr_decay, [int(v) for v in sys.argv[7].split(",")], sys.argv[6])
@@ -161,6 +166,7 @@ def main():
     out_path = Path(sys.argv[4]) if len(sys.argv) > 4 else ROOT / "profiles" / "r02_psnr_parity.json"
     lr_decay = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     n_workers = int(sys.argv[6]) if len(sys.argv) > 6 else 1
+    first = int(sys.argv[7]) if len(sys.argv) > 7 else 0
     batch = 1024
     # Training at constant Adam LR is chaotic: a 1-ulp difference anywhere decorrelates two
     # trajectories within a few hundred steps, so one run of each says nothing at 0.1 dB.
@@ -173,7 +179,7 @@ def main():
     tmp = Path(tempfile.mkdtemp())
     procs = []
     for w in range(n_workers):
-        seeds = list(range(w, n_seeds, n_workers))
+        seeds = list(range(first + w, first + n_seeds, n_workers))
         if seeds:
             procs.append(subprocess.Popen([sys.executable, "-u", __file__, "--worker", str(iters), str(size),
                                            str(batch), str(lr_decay), str(tmp / f"w{w}.jsonl"),
@@ -230,6 +236,25 @@ def summarize_results(results, iters, size, batch, n_seeds, lr_decay, out_path, 
     print(json.dumps(delta))
 
 
+
+
+def merge(out_path, paths):
+    """One record from several of the same setup (iters, size, batch, lr_decay) whose
+    seed ranges are disjoint: the pooled runs, re-summarised as one paired comparison."""
+    recs = [json.loads(p.read_text()) for p in paths]
+    keys = ("iters", "size", "batch", "lr_decay")
+    if any(tuple(r[k] for k in keys) != tuple(recs[0][k] for k in keys) for r in recs):
+        raise SystemExit("psnr_parity --merge: records of different setups")
+    results = [x for r in recs for x in r["results"]]
+    seen = {}
+    for x in results:
+        k = (x["impl"], x["precision"], x["seed"])
+        if k in seen:
+            raise SystemExit(f"psnr_parity --merge: seed {x['seed']} appears twice for {x['impl']}/{x['precision']}")
+        seen[k] = x
+    note = "pooled from " + ", ".join(f"{p.name} (commit {r.get('commit')})" for p, r in zip(paths, recs))
+    r0 = recs[0]
+    summarize_results(results, r0["iters"], r0["size"], r0["batch"], None, r0["lr_decay"], out_path, note=note)
 
 
 def from_log(log_path, out_path, iters=2000, size=64, batch=1024, lr_decay=1, note=None):
