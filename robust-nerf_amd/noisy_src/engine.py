@@ -188,11 +188,13 @@ class GradAllReducer:
 
 class Trainer:
     """One reference training iteration (train.py:68-119) on the HIP kernels.
-    ``coarse_stream``: run the coarse network's forward, compositing and (through
-    autograd's stream semantics) their backward on a second stream beside the fine
-    network's; bit-identical to the one-stream step.  It pays where one chain does not
-    fill the GPU (BASELINE cfg #4's 512 rays per rank; inside a GraphedTrainer capture the
-    two chains become two branches of the graph)."""
+    ``coarse_stream``: run the coarse network's forward, compositing, loss and backward on
+    a second stream; the coarse backward starts as soon as the coarse forward ends and
+    runs beside the fine sampling, forward and backward (the fine samples depend on the
+    coarse weights only through detached z values, rays.py:325, so d(loss_c + loss_f)
+    reaches the coarse net as d loss_c alone).  Bit-identical to the one-stream step.  It
+    pays where one chain does not fill the GPU (BASELINE cfg #4's 512 rays per rank; inside
+    a GraphedTrainer capture the two chains become two branches of the graph)."""
 
     def __init__(self, model_coarse, model_fine, render_config, lr: float = 5e-4, lr_decay: int = 250,
                  max_norm: float = 1.0, process_group=None, coarse_stream: bool = False):
@@ -224,19 +226,34 @@ class Trainer:
             if self._cstream is None or self._cstream.device != rays_o.device:
                 self._cstream = torch.cuda.Stream(device=rays_o.device)
             cs = self._cstream
-        out = render_rays(self.model_coarse, self.model_fine, rays_o, rays_d, self.render_config, is_train=True,
-                          t_rand=t_rand, u=u, coarse_stream=cs)
         gs = self.reducer.prescale if self.reducer is not None else 1.0  # DP: 1/world in the seed
-        loss_c = ops.mse_loss(out["rgb_coarse"], target_rgb, gs)
-        loss = loss_c
-        metrics = {"loss_coarse": loss_c.detach()}  # metrics hold no autograd graph
-        if "rgb_fine" in out:
-            loss_f = ops.mse_loss(out["rgb_fine"], target_rgb, gs)
-            loss = loss_c + loss_f
-            metrics["loss_fine"] = loss_f.detach()
-        loss.backward(ops.unit_grad(loss.device))
+        early = {}
+
+        def coarse_backward(out_c):
+            # on the coarse stream: the coarse loss and its backward, beside the fine
+            # forward (loss = loss_c + loss_f sends exactly d loss_c to the coarse net)
+            early["loss_c"] = ops.mse_loss(out_c["rgb_map"], target_rgb, gs)
+            early["loss_c"].backward(ops.unit_grad(rays_o.device))
+
+        out = render_rays(self.model_coarse, self.model_fine, rays_o, rays_d, self.render_config, is_train=True,
+                          t_rand=t_rand, u=u, coarse_stream=cs,
+                          coarse_backward=coarse_backward if cs is not None else None)
         if cs is not None:
-            torch.cuda.current_stream(rays_o.device).wait_stream(cs)  # join the coarse chain's backward
+            loss_f = ops.mse_loss(out["rgb_fine"], target_rgb, gs)
+            loss_f.backward(ops.unit_grad(rays_o.device))
+            torch.cuda.current_stream(rays_o.device).wait_stream(cs)  # join the coarse chain
+            loss_c = early["loss_c"].detach()
+            loss = loss_c + loss_f.detach()  # the backward already ran: the value only
+            metrics = {"loss_coarse": loss_c.detach(), "loss_fine": loss_f.detach()}
+        else:
+            loss_c = ops.mse_loss(out["rgb_coarse"], target_rgb, gs)
+            loss = loss_c
+            metrics = {"loss_coarse": loss_c.detach()}  # metrics hold no autograd graph
+            if "rgb_fine" in out:
+                loss_f = ops.mse_loss(out["rgb_fine"], target_rgb, gs)
+                loss = loss_c + loss_f
+                metrics["loss_fine"] = loss_f.detach()
+            loss.backward(ops.unit_grad(loss.device))
         if self.reducer is not None:
             flats = [flat for _, flat in self.reducer.pending]
             self.reducer.finish()

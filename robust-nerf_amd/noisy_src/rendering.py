@@ -9,7 +9,7 @@ sampling -> fused MLP -> composite exactly as rendering.py:119-240 does, and
 
 from __future__ import annotations
 
-from typing import Dict, Optional
+from typing import Callable, Dict, Optional
 
 import torch
 import torch.nn as nn
@@ -43,7 +43,9 @@ def raw2outputs(rgb: torch.Tensor, sigma: torch.Tensor, z_vals: torch.Tensor, ra
 def render_rays(model_coarse: NeRF, model_fine: Optional[NeRF], rays_o: torch.Tensor, rays_d: torch.Tensor,
                 config: RenderConfig, is_train: bool = True, t_rand: Optional[torch.Tensor] = None,
                 u: Optional[torch.Tensor] = None, return_aux: bool = False,
-                coarse_stream: Optional[torch.cuda.Stream] = None) -> Dict[str, torch.Tensor]:
+                coarse_stream: Optional[torch.cuda.Stream] = None,
+                coarse_backward: Optional[Callable[[Dict[str, torch.Tensor]], None]] = None
+                ) -> Dict[str, torch.Tensor]:
     """Reference rendering.py:119-240.  ``t_rand`` / ``u`` inject the jitter and
     inverse-CDF uniforms (otherwise drawn with torch.rand as the reference does).
 
@@ -52,7 +54,10 @@ def render_rays(model_coarse: NeRF, model_fine: Optional[NeRF], rays_o: torch.Te
     there too, beside the fine network's (the two chains are independent: the fine
     samples depend on the coarse weights only through detached z values, reference
     rays.py:325).  Same kernels, same results; the caller joins the stream after
-    ``backward``."""
+    ``backward``.  ``coarse_backward(out_c)``, with a coarse stream: called on that stream
+    right after the coarse compositing (the caller runs the coarse loss's backward there),
+    and the current stream waits only for the coarse FORWARD, so the coarse backward runs
+    beside the fine sampling and forward."""
     perturb = config.perturb if is_train else False
     raw_noise_std = config.raw_noise_std if is_train else 0.0
     N_rays = rays_o.shape[0]
@@ -69,7 +74,13 @@ def render_rays(model_coarse: NeRF, model_fine: Optional[NeRF], rays_o: torch.Te
             rgb_c, sigma_c = model_coarse(pts.reshape(-1, 3), vd)
             out_c = raw2outputs(rgb_c.reshape(N_rays, Nc, 3), sigma_c.reshape(N_rays, Nc, 1), z_c, rays_d,
                                 raw_noise_std=raw_noise_std, white_background=config.white_background)
-        main.wait_stream(coarse_stream)
+            if coarse_backward is not None:
+                forward_done = coarse_stream.record_event()
+                coarse_backward(out_c)
+        if coarse_backward is not None:
+            main.wait_event(forward_done)
+        else:
+            main.wait_stream(coarse_stream)
     else:
         rgb_c, sigma_c = model_coarse(pts.reshape(-1, 3), vd)
         out_c = raw2outputs(rgb_c.reshape(N_rays, Nc, 3), sigma_c.reshape(N_rays, Nc, 1), z_c, rays_d,

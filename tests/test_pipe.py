@@ -17,10 +17,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _net(precision, skips=(4,), use_view_dirs=True, layers=8, seed=0):
+def _net(precision, skips=(4,), use_view_dirs=True, layers=8, seed=0, **extra):
     from noisy_src.config import ModelConfig
     from noisy_src.model import NeRF
-    cfg = ModelConfig(precision=precision, skips=skips, use_view_dirs=use_view_dirs, num_hidden_layers=layers)
+    cfg = ModelConfig(precision=precision, skips=skips, use_view_dirs=use_view_dirs, num_hidden_layers=layers,
+                      **extra)
     torch.manual_seed(seed)
     return NeRF(cfg).to(DEV)
 
@@ -110,6 +111,9 @@ def test_fused_input_gradients_pose_mode():
 
 
 def test_outside_envelope_runs_split():
-    """fp32 and two-skip models are not pipelined: dxdw runs the split form (same result)."""
+    """fp32, two-skip and one-block-x_enc models (pos_freqs 4: no pipelined kernel
+    instance) are not pipelined: dxdw runs the split form (same result), and
+    nr_mlp_backward_pipelined says so."""
     _check(_net("fp32"), 5000, expect_pipe=False)
+    _check(_net("bf16", pos_freqs=4), 5000, expect_pipe=False)
     _check(_net("bf16", layers=7, skips=(2, 5)), 5000, expect_pipe=False)
