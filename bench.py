@@ -482,9 +482,10 @@ def main():
                          "data parallelism the RCCL all-reduces are captured too)")
     ap.add_argument("--dp", action="store_true",
                     help="join an RCCL process group even at N=1 (the data-parallel step, all-reduce hooks active)")
-    ap.add_argument("--coarse-stream", action="store_true",
-                    help="run the coarse network's chain on a second stream beside the fine one "
-                         "(engine.Trainer(coarse_stream=True); with --graph: two branches of the graph)")
+    ap.add_argument("--coarse-stream", nargs="?", const="on", default="auto", choices=("auto", "on", "off"),
+                    help="run the coarse network's chain (forward, loss, backward) on a second stream beside "
+                         "the fine one (engine.Trainer(coarse_stream=...); with --graph: two branches of the "
+                         "graph); auto (default): only in a graph replay of <= 1024 rays, where it pays")
     ap.add_argument("--pose-opt", action="store_true",
                     help="BASELINE cfg #3: joint pose optimisation step (train_pose_opt, poses optimising)")
     args = ap.parse_args()
@@ -551,6 +552,10 @@ def main():
         sl = slice(rank * B, (rank + 1) * B)
     else:
         B = args.batch
+    # engine.Trainer's rule for "auto": a graph replay of <= AUTO_COARSE_STREAM_RAYS rays
+    coarse_stream_used = not args.pose_opt and (
+        args.coarse_stream == "on" or (args.coarse_stream == "auto" and args.graph
+                                       and B <= Trainer.AUTO_COARSE_STREAM_RAYS))
     if args.pose_opt:
         # rays come from (image, pixel) and the learnable poses INSIDE the step; the
         # pixel draws (sampler.sample_batch) stay outside it, as batch sampling does below
@@ -565,7 +570,8 @@ def main():
             gen = torch.Generator(device=dev).manual_seed(1000 * rank)
             pool = [sampler.sample_batch(generator=gen) for _ in range(4)]
     else:
-        trainer = Trainer(mc, mf, rcfg, process_group=pg, coarse_stream=args.coarse_stream)
+        trainer = Trainer(mc, mf, rcfg, process_group=pg,
+                          coarse_stream={"auto": "auto", "on": True, "off": False}[args.coarse_stream])
         if strong:
             pool = [tuple(x[sl] for x in lego_rays(args.global_batch, 1000 + k, dev)) for k in range(4)]
         else:
@@ -689,7 +695,7 @@ def main():
             "parallelism": f"dp{world}" + (" (RCCL process group, all-reduce in the step)" if pg is not None
                                            and world == 1 else ""),
             **({"execution": "hipGraph replay (engine.GraphedTrainer)"} if args.graph else {}),
-            **({"coarse_stream": "coarse chain on a second stream"} if args.coarse_stream else {}),
+            **({"coarse_stream": "coarse chain on a second stream"} if coarse_stream_used else {}),
         },
         # headline: the dominant kernel on SURVEY §8d's MFMA basis (algorithmic FLOPs per
         # launch over its launch time); the stored-activation HBM view rides beside it

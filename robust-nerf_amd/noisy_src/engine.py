@@ -193,11 +193,19 @@ class Trainer:
     runs beside the fine sampling, forward and backward (the fine samples depend on the
     coarse weights only through detached z values, rays.py:325, so d(loss_c + loss_f)
     reaches the coarse net as d loss_c alone).  Bit-identical to the one-stream step.  It
-    pays where one chain does not fill the GPU (BASELINE cfg #4's 512 rays per rank; inside
-    a GraphedTrainer capture the two chains become two branches of the graph)."""
+    pays where one chain does not fill the GPU and the host is out of the way: inside a
+    GraphedTrainer capture (the two chains become two branches of the graph) at up to
+    ``AUTO_COARSE_STREAM_RAYS`` rays per step (BASELINE cfg #4's 512 rays per rank: 0.856
+    -> 0.802 ms per replay; 1024 rays 1.36 -> 1.34 ms; 2048 and 4096 rays no gain or a
+    loss; eager steps lose to the second stream's host cost, profiles/r05_coarse_early_ab.txt).
+    ``coarse_stream="auto"`` applies exactly that rule per step; True / False force it."""
+
+    AUTO_COARSE_STREAM_RAYS = 1024
 
     def __init__(self, model_coarse, model_fine, render_config, lr: float = 5e-4, lr_decay: int = 250,
-                 max_norm: float = 1.0, process_group=None, coarse_stream: bool = False):
+                 max_norm: float = 1.0, process_group=None, coarse_stream=False):
+        if coarse_stream not in (True, False, "auto"):
+            raise ValueError(f"coarse_stream must be True, False or 'auto', not {coarse_stream!r}")
         self.coarse_stream = coarse_stream
         self._cstream = None
         self.model_coarse = model_coarse
@@ -222,7 +230,11 @@ class Trainer:
              t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         self.optimizer.zero_grad(set_to_none=True)
         cs = None
-        if self.coarse_stream and self.model_fine is not None and rays_o.is_cuda:
+        want = self.coarse_stream
+        if want == "auto":
+            want = (rays_o.is_cuda and rays_o.shape[0] <= self.AUTO_COARSE_STREAM_RAYS
+                    and torch.cuda.is_current_stream_capturing())
+        if want and self.model_fine is not None and rays_o.is_cuda:
             if self._cstream is None or self._cstream.device != rays_o.device:
                 self._cstream = torch.cuda.Stream(device=rays_o.device)
             cs = self._cstream

@@ -229,8 +229,10 @@ def train(config: NeRFConfig, noise_config: Optional[NoiseConfig] = None, *,
         if model_fine is not None:
             logger.log_model_info(model_fine, "model_fine")
     renderer = NeRFRenderer(model_coarse, model_fine, config.render)
+    # coarse_stream="auto": the coarse chain becomes a second graph branch only in a
+    # --graph replay of <= 1024 rays (engine.Trainer), where it pays
     trainer = Trainer(model_coarse, model_fine, config.render, lr=config.train.lr, lr_decay=config.train.lr_decay,
-                      process_group=process_group)
+                      process_group=process_group, coarse_stream="auto")
     optimizer = trainer.optimizer
     lpips_metric = LPIPSMetric(device=device) if rank == 0 else None
     if lpips_metric is not None and not lpips_metric.available:
