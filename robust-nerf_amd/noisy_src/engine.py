@@ -206,8 +206,9 @@ class Trainer:
                  max_norm: float = 1.0, process_group=None, coarse_stream=False):
         if coarse_stream not in (True, False, "auto"):
             raise ValueError(f"coarse_stream must be True, False or 'auto', not {coarse_stream!r}")
-        self.coarse_stream = coarse_stream
+        self.coarse_stream = coarse_stream if coarse_stream == "auto" else bool(coarse_stream)
         self._cstream = None
+        self.last_step_coarse_stream = False  # whether the last step (or capture) used it
         self.model_coarse = model_coarse
         self.model_fine = model_fine
         self.render_config = render_config
@@ -230,14 +231,15 @@ class Trainer:
              t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         self.optimizer.zero_grad(set_to_none=True)
         cs = None
-        want = self.coarse_stream
-        if want == "auto":
-            want = (rays_o.is_cuda and rays_o.shape[0] <= self.AUTO_COARSE_STREAM_RAYS
-                    and torch.cuda.is_current_stream_capturing())
-        if want and self.model_fine is not None and rays_o.is_cuda:
+        if self.coarse_stream is not False and self.model_fine is not None and rays_o.is_cuda:
+            # created on the first eager step (a GraphedTrainer warms up eagerly), not
+            # inside a capture
             if self._cstream is None or self._cstream.device != rays_o.device:
                 self._cstream = torch.cuda.Stream(device=rays_o.device)
-            cs = self._cstream
+            if self.coarse_stream is True or (rays_o.shape[0] <= self.AUTO_COARSE_STREAM_RAYS
+                                              and torch.cuda.is_current_stream_capturing()):
+                cs = self._cstream
+        self.last_step_coarse_stream = cs is not None
         gs = self.reducer.prescale if self.reducer is not None else 1.0  # DP: 1/world in the seed
         early = {}
 

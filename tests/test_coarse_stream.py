@@ -70,3 +70,41 @@ def test_coarse_stream_graph_equals_eager():
         lg = float(graphed.step(*b)["loss"])
         assert le == lg, (k, le, lg)
     _same(one, two)
+
+
+def test_auto_engages_only_in_small_graph_replays():
+    """coarse_stream="auto" (bench.py / train.py default): eager steps stay on one stream;
+    a GraphedTrainer capture of <= AUTO_COARSE_STREAM_RAYS rays gets the second branch,
+    and its replays equal the one-stream eager step bit for bit."""
+    from noisy_src.config import ModelConfig, RenderConfig
+    from noisy_src.engine import GraphedTrainer, Trainer
+    from noisy_src.model import create_nerf
+    rc = RenderConfig(num_samples=64, num_samples_fine=128)
+    torch.manual_seed(17)
+    mc, mf = create_nerf(ModelConfig(precision="bf16"))
+    one = Trainer(mc.to(DEV), mf.to(DEV), rc, coarse_stream=False)
+    torch.manual_seed(17)
+    mc, mf = create_nerf(ModelConfig(precision="bf16"))
+    auto = Trainer(mc.to(DEV), mf.to(DEV), rc, coarse_stream="auto")
+    bs = _batches(rc, 512, 5)
+    assert 512 <= Trainer.AUTO_COARSE_STREAM_RAYS
+    auto.step(*bs[0])
+    assert not auto.last_step_coarse_stream  # eager: one stream
+    one.step(*bs[0])
+    graphed = GraphedTrainer(auto, *bs[1], warmup=1)
+    one.step(*bs[1])
+    assert auto.last_step_coarse_stream  # the capture took the two-branch form
+    for k, b in enumerate(bs[2:]):
+        le = float(one.step(*b)["loss"])
+        lg = float(graphed.step(*b)["loss"])
+        assert le == lg, (k, le, lg)
+    _same(one, auto)
+
+
+def test_coarse_stream_rejects_unknown_mode():
+    from noisy_src.config import ModelConfig, RenderConfig
+    from noisy_src.engine import Trainer
+    from noisy_src.model import create_nerf
+    mc, mf = create_nerf(ModelConfig(precision="bf16"))
+    with pytest.raises(ValueError, match="coarse_stream"):
+        Trainer(mc, mf, RenderConfig(), coarse_stream="sometimes")
