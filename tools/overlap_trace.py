@@ -54,6 +54,10 @@ def main(trace_dir: str, out: str | None = None) -> None:
                                  f"{(x[0] - t0) / 1e3:.1f}-{(x[1] - t0) / 1e3:.1f}"
                                  for x in sorted(rccl + co))
                      + f"; first all-reduce kernel starts before the coarse dW ends: {overlap}")
+    if not any("nccl" in x[2].lower() for x in recs):
+        lines.append("no RCCL kernel in this trace: a one-rank communicator completes an all-reduce without "
+                     "launching one, so the overlap shows only in a multi-rank run (bench.py's topology "
+                     "fields time the all-reduce with HIP events at any world size)")
     lines.append(f"{n_overlap} of {n_steps} steps: the first RCCL kernel starts before the coarse backward's dW "
                  f"kernel ends (coarse M={m_coarse}, fine M={m_fine})")
     text = "\n".join(lines)
