@@ -221,9 +221,10 @@ def rank_topology(pg, dev, step_ms_median: float, allreduce):
     return {"backend": dist.get_backend(pg), "world_size": dist.get_world_size(pg),
             "distinct_devices": len({(r["pci_bus_id"], r["pci_device_id"], r["device"]) for r in ranks}),
             "allreduce_steps": allreduce["steps"] if allreduce else 0,
-            "allreduce_note": "HIP events on the compute stream: span = first gradient all-reduce launched "
-                              "(fine net, during the coarse backward) -> all reduced; exposed = the step's wait "
-                              "for it in GradAllReducer.finish" if allreduce else "graph replay: not timed",
+            "allreduce_note": "HIP events on the compute stream over the last warm-up steps (eager; outside the "
+                              "timed region): span = first gradient all-reduce launched (fine net, during the "
+                              "coarse backward) -> all reduced; exposed = the step's wait for it in "
+                              "GradAllReducer.finish" if allreduce else "not timed (fewer than 2 warm-up steps)",
             "ranks": ranks}
 
 
@@ -590,12 +591,21 @@ def main():
     mlp_entries = ["nr_mlp_forward", "nr_mlp_backward_dx", "nr_mlp_backward_dw", "nr_mlp_backward_dxdw",
                    "nr_mlp_backward_reduce"]
     wtimer = _hip.CallTimer(mlp_entries)
+    # the data-parallel all-reduce is timed over the same warm-up steps (HIP events around
+    # GradAllReducer's launch and wait), not inside the timed region: at small host-bound
+    # batches the extra event records would lengthen the measured steps
+    reducer = getattr(trainer, "reducer", None)
     for k in range(args.warmup):
         if k == args.warmup // 2:
             _hip.set_timer(wtimer)
+            if reducer is not None:
+                reducer.timing = []
         step(k)
     _hip.set_timer(None)
     torch.cuda.synchronize()
+    ar_timing = reducer.timing_summary() if reducer is not None else None
+    if reducer is not None:
+        reducer.timing = None
     wcalls = wtimer.summary()
     # dominant kernel = largest total time per step (no warm-up: time them all live)
     dom_key = max(wcalls, key=lambda k: wcalls[k][0] * wcalls[k][1]) if wcalls else None
@@ -617,9 +627,6 @@ def main():
             step(k)
     timer = _hip.CallTimer(mlp_entries, keys=[dom_key] if dom_key else None)
     _hip.set_timer(timer)
-    reducer = getattr(trainer, "reducer", None)
-    if reducer is not None and not args.graph:
-        reducer.timing = []  # HIP events around every step's all-reduce wait (eager steps)
     if pg is not None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -646,9 +653,7 @@ def main():
     step_pcts = [round(per_step[min(len(per_step) - 1, int(q * len(per_step)))], 4) for q in (0.1, 0.5, 0.9)]
     topology = None
     if pg is not None:
-        topology = rank_topology(pg, dev, step_pcts[1], reducer.timing_summary() if reducer is not None else None)
-        if reducer is not None:
-            reducer.timing = None
+        topology = rank_topology(pg, dev, step_pcts[1], ar_timing)
     calls = timer.summary() if not args.graph else {dom_key: wcalls[dom_key]}
     if dom_key is None:
         wcalls = calls
