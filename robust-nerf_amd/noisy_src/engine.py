@@ -526,14 +526,18 @@ def _adopt_reduced_grad(net, flats) -> None:
     g = _contiguous_run([p.grad for p in net.parameters()])
     if g is not None and any(g.data_ptr() == f.data_ptr() for f in flats):
         return
-    for f in flats:
+    # this net's own flat gradient (the coarse and fine nets have equal sizes, and with a
+    # coarse stream the coarse all-reduce may be launched first)
+    last = getattr(net, "_last_gflat", None)
+    mine = [f for f in flats if last is not None and f.data_ptr() == last.data_ptr()]
+    for f in mine or flats:
         if f.numel() == net._param_count:
             off = 0
             for p in net.parameters():
                 n = p.numel()
                 p.grad.copy_(f[off:off + n].view(p.shape))
                 off += n
-            flats.remove(f)
+            del flats[next(i for i, x in enumerate(flats) if x is f)]  # by identity (== is elementwise)
             return
 
 
