@@ -387,11 +387,19 @@ class GraphedTrainer:
         """Replay one training step on these rays (copied into the static buffers; None:
         the buffers as they are).  Returns the captured metrics (device tensors that every
         replay overwrites).  Eager ``trainer.step`` calls may be interleaved (same state)."""
+        dsts, srcs = [], []
         for dst, src in zip(self.static + self.static_rand, (rays_o, rays_d, target_rgb, t_rand, u)):
             if src is not None:
                 if dst is None:
                     raise ValueError("GraphedTrainer: t_rand / u were drawn in the graph at capture")
-                dst.copy_(src)
+                dsts.append(dst)
+                srcs.append(src)
+        if dsts and all(x.is_cuda and x.device == d.device and x.dtype == d.dtype and x.shape == d.shape
+                        for d, x in zip(dsts, srcs)):
+            torch._foreach_copy_(dsts, srcs)  # one launch for all the static inputs
+        else:
+            for d, x in zip(dsts, srcs):
+                d.copy_(x)
         self._check_bound()
         opt = self.trainer.optimizer
         group = opt.param_groups[0]
