@@ -46,3 +46,26 @@ def test_recorded_psnr_parity_meets_the_bar(impl):
     d = rec["delta_vs_ref"][impl]
     assert abs(d["paired_mean_db"]) + 2 * d["paired_se_db"] <= 0.11, d
     assert d["paired_se_db"] <= 0.05, d
+
+
+def test_merge_pools_disjoint_seed_ranges(tmp_path):
+    """psnr_parity --merge: two records of one setup with disjoint seeds give the pooled
+    paired statistics; a seed present in both is refused."""
+    mod = _mod()
+
+    def rec(seeds, path):
+        res = [{"impl": i, "precision": p, "seed": s, "test_psnr": 30.0 + s + d, "per_view": None, "iters": 10,
+                "batch": 4, "size": 8, "train_seconds": 1.0}
+               for s in seeds for (i, p), d in zip(mod.IMPLS, (0.0, 0.1, -0.2))]
+        mod.summarize_results(res, 10, 8, 4, None, 250, path)
+
+    rec([0, 1, 2], tmp_path / "a.json")
+    rec([3, 4], tmp_path / "b.json")
+    mod.merge(tmp_path / "m.json", [tmp_path / "a.json", tmp_path / "b.json"])
+    m = json.loads((tmp_path / "m.json").read_text())
+    assert m["seeds"] == 5 and m["lr_decay"] == 250
+    assert m["delta_vs_ref"]["hip_fp32"]["paired_mean_db"] == pytest.approx(0.1)
+    assert m["delta_vs_ref"]["hip_bf16"]["paired_mean_db"] == pytest.approx(-0.2)
+    rec([2, 5], tmp_path / "c.json")
+    with pytest.raises(SystemExit, match="twice"):
+        mod.merge(tmp_path / "x.json", [tmp_path / "a.json", tmp_path / "c.json"])
