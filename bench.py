@@ -281,7 +281,10 @@ def psnr_record():
                 "lr_decay": rec.get("lr_decay"),
                 "paired_delta_db_vs_ref": {k: v.get("paired_mean_db", v["delta_mean_db"])
                                            for k, v in rec["delta_vs_ref"].items()},
-                "paired_se_db": {k: v.get("paired_se_db", v["se_of_delta_db"]) for k, v in rec["delta_vs_ref"].items()}}
+                "paired_se_db": {k: v.get("paired_se_db", v["se_of_delta_db"]) for k, v in rec["delta_vs_ref"].items()},
+                **({"paired_ci90_db": {k: v["paired_ci90_db"] for k, v in rec["delta_vs_ref"].items()},
+                    "within_0p1_db_tost": {k: v["within_0p1_db_tost"] for k, v in rec["delta_vs_ref"].items()}}
+                   if all("paired_ci90_db" in v for v in rec["delta_vs_ref"].values()) else {})}
     recs = [(f, json.loads(f.read_text()).get("lr_decay")) for f in sorted((ROOT / "profiles").glob("r*_psnr_parity*.json"))]
     main = [f for f, ld in recs if ld in (1, None)]
     ref = [f for f, ld in recs if ld == 250]

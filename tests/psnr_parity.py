@@ -209,9 +209,16 @@ def summarize_results(results, iters, size, batch, n_seeds, lr_decay, out_path, 
         se = math.sqrt(summ[k]["sem"] ** 2 + base["sem"] ** 2)
         paired = [a["test_psnr"] - b["test_psnr"] for a, b in zip(groups[k], groups["ref_fp32"])]
         pse = float(np.std(paired, ddof=1) / math.sqrt(len(paired))) if len(paired) > 1 else 0.0
+        pm = float(np.mean(paired))
         delta[k] = {"delta_mean_db": round(d, 4), "se_of_delta_db": round(se, 4),
-                    "paired_mean_db": round(float(np.mean(paired)), 4), "paired_se_db": round(pse, 4),
+                    "paired_mean_db": round(pm, 4), "paired_se_db": round(pse, 4),
                     "z": round(d / se, 3) if se > 0 else None,
+                    # paired 95 % interval, and the two one-sided tests at 5 % each (TOST)
+                    # for |delta| < 0.1 dB: equivalent iff the 90 % interval lies inside
+                    "paired_ci95_db": [round(pm - 1.96 * pse, 4), round(pm + 1.96 * pse, 4)],
+                    "paired_ci90_db": [round(pm - 1.645 * pse, 4), round(pm + 1.645 * pse, 4)],
+                    "within_0p1_db_tost": bool(len(paired) > 1 and pm - 1.645 * pse > -0.1
+                                               and pm + 1.645 * pse < 0.1),
                     "paired_deltas_db": [round(x, 4) for x in paired]}
     import os
     import subprocess
