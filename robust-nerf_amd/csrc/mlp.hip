@@ -1688,7 +1688,7 @@ struct DwArgs {
     uint16_t wg_map[kDwMaxWgs];     // workgroup -> job | chunk << 5 (chunk-major: one chunk of every job in a row)
     int stage_bytes, nstage;
     int64_t slab_floats_per_chunk;
-    int job_NBz[kMaxJobs], job_KB[kMaxJobs], job_nseg[kMaxJobs];
+    int job_NBz[kMaxJobs], job_KB[kMaxJobs];
     int64_t job_slab[kMaxJobs];
     const char* seg_ptr[kMaxJobs][2 * kMaxJobSeg];  // tensor region: dz segments, then inputs
     uint8_t seg_blocks[kMaxJobs][2 * kMaxJobSeg];
@@ -1786,7 +1786,6 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     if (t1 > a.tiles) t1 = a.tiles;
     constexpr int FPB = kFPB<PREC>;
     constexpr int BLK = FPB * kFragBytes;
-    const int nseg = a.job_nseg[j];
 
     // Stage tile t into buffer b (the job's blocks, dz segments first).  Every wave
     // issues exactly `per_wave` 1-KB LDS-DMA pieces per tile (padding pieces re-load
@@ -3128,7 +3127,6 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
             w.seg_ptr[j][ns] = (jb.in[q].is_ws ? ws : sv) + (jb.in[q].is_ws ? z.ws_off : z.saved_off)[jb.in[q].tensor];
             w.seg_blocks[j][ns] = static_cast<uint8_t>(jb.in[q].blocks);
         }
-        w.job_nseg[j] = ns;
         w.job_slab[j] = jb.slab_off;
         NR_REQUIRE((jb.NBz + jb.KB) * p.fpb <= kDwWaves * dw_max_pieces(p.fpb == 2),
                    "nr_mlp_backward_dw: job %d stages %d blocks, beyond the kernel's per-wave pieces", j, jb.NBz + jb.KB);
