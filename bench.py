@@ -285,9 +285,14 @@ def psnr_record():
                 **({"paired_ci90_db": {k: v["paired_ci90_db"] for k, v in rec["delta_vs_ref"].items()},
                     "within_0p1_db_tost": {k: v["within_0p1_db_tost"] for k, v in rec["delta_vs_ref"].items()}}
                    if all("paired_ci90_db" in v for v in rec["delta_vs_ref"].values()) else {})}
-    recs = [(f, json.loads(f.read_text()).get("lr_decay")) for f in sorted((ROOT / "profiles").glob("r*_psnr_parity*.json"))]
-    main = [f for f, ld in recs if ld in (1, None)]
-    ref = [f for f, ld in recs if ld == 250]
+    # per schedule, the record with the most seeds (then the latest name): pooled records
+    # (tests/psnr_parity.py --merge) supersede the batches they pool
+    recs = []
+    for f in sorted((ROOT / "profiles").glob("r*_psnr_parity*.json")):
+        r = json.loads(f.read_text())
+        recs.append((r.get("seeds") or 0, f.name, f, r.get("lr_decay")))
+    main = [f for _, _, f, ld in sorted(recs) if ld in (1, None)]
+    ref = [f for _, _, f, ld in sorted(recs) if ld == 250]
     out = one(main[-1]) if main else None
     if out is not None and ref:
         out["reference_schedule"] = one(ref[-1])
