@@ -51,9 +51,7 @@ DW_FEATURES = (63 + 8 * 256 + 256 + 27 + 128) + (8 * 256 + 256 + 128 + 1 + 3)
 # kernels behind each entry point (16-bit forward / dX: the row-block-major kernels)
 KERNEL_OF = {"nr_mlp_forward": ("mlp_fwd_rbm_kernel", "mlp_fwd_kernel"),
              "nr_mlp_backward_dx": ("mlp_bwd_rbm_kernel", "mlp_bwd_kernel"),
-             "nr_mlp_backward_dw": ("mlp_dw_kernel",), "nr_mlp_backward_reduce": ("mlp_dw_reduce_kernel",),
-             # opt-in fused layer-pipelined backward (NR_MLP_BACKWARD=fused, csrc/mlp_pipe.inc)
-             "nr_mlp_backward_dxdw": ("mlp_bwd_pipe_kernel",)}
+             "nr_mlp_backward_dw": ("mlp_dw_kernel",), "nr_mlp_backward_reduce": ("mlp_dw_reduce_kernel",)}
 
 
 def traffic_of(kernels, M: int, prec: str):
@@ -93,7 +91,9 @@ def rocprof_summary(prec: str):
         rows = {}
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if r.get("source_hash") != want:
+                # a summary stamped with an overridden hash (NR_SOURCE_HASH) is not a
+                # same-source measurement
+                if r.get("source_hash") != want or r.get("hash_overridden"):
                     break
                 if r.get("M_samples") and r.get("precision", prec) == prec:
                     rows[(r["kernel"], int(r["M_samples"]))] = r
@@ -129,8 +129,8 @@ def bound_of(entry: str, M: int, prec: str, counted_bytes):
 def mfma_macs_of(entry: str) -> int:
     """MFMA multiply-adds per sample of one fused-MLP launch (SURVEY.md §8d basis): the
     forward's layers, the dX chain's W^T products, dW's outer products (one per weight)."""
-    return {"nr_mlp_forward": MACS_PER_EVAL, "nr_mlp_backward_dx": MACS_DX, "nr_mlp_backward_dw": MACS_PER_EVAL,
-            "nr_mlp_backward_dxdw": MACS_DX + MACS_PER_EVAL}.get(entry, 0)
+    return {"nr_mlp_forward": MACS_PER_EVAL, "nr_mlp_backward_dx": MACS_DX,
+            "nr_mlp_backward_dw": MACS_PER_EVAL}.get(entry, 0)
 
 
 def mfma_roofline(entry: str, M: int, ms: float, prec: str):
@@ -163,37 +163,52 @@ def roofline_of(entry: str, M: int, ms: float, prec: str, n_params: int, counted
     return "hbm", nbytes / (ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s", f"{n_params} fp32 grads"
 
 
-def kernel_table(wcalls, prec: str, n_params: int, steps_per_key=1):
-    """Per fused-MLP launch key: live ms, counted HBM bytes (PMC), the counted-byte rate,
-    MFMA / HBM floors and the bound; plus the step's counted MLP bytes."""
+def kernel_table(wcalls, prec: str, n_params: int, rp_rows=None, active=None):
+    """Per fused-MLP launch key: its launch ms, counted HBM bytes (PMC), the counted-byte
+    rate, MFMA / HBM floors and the bound; plus the step's counted MLP bytes.  The ms is the
+    committed same-source rocprof timed-region average (``ms_source`` "rocprof") when one
+    exists for the key -- the headline's basis, so every fraction here agrees with it and
+    the launches sum to at most the step -- else the HIP-event-bracketed warm-up mean,
+    labelled "bracketed" and given no fractions (a bracketed launch carries queue gaps).
+    ``active``: {M: active-tile fraction}; MFMA fractions count the executed tiles."""
     out, step_bytes = {}, 0.0
-    for key, (n, ms) in sorted(wcalls.items()):
+    for key, (n, live_ms) in sorted(wcalls.items()):
         entry, M = key.split("[M=")[0], int(key.split("[M=")[1].rstrip("]"))
         kern = KERNEL_OF.get(entry, (entry,))
+        rp = next((rp_rows[(k, M)] for k in kern if rp_rows and (k, M) in rp_rows), None)
+        rp_ms = float(rp.get("timed_avg_ms") or rp["avg_ms"]) if rp else None
+        ms = rp_ms if rp_ms else live_ms
         tb = traffic_of(kern, M, prec if entry != "nr_mlp_backward_reduce" else "")
         bound, f_mfma, f_hbm = bound_of(entry, M, prec, tb)
-        rec = {"ms": round(ms, 4), "bound": bound, "mfma_floor_ms": round(f_mfma, 4), "hbm_floor_ms": round(f_hbm, 4)}
-        fl = _flops_of(entry, M)
-        if fl:
-            rec["mfma_tflops"] = round(fl / (ms * 1e-3) / 1e12, 1)
-            rec["mfma_frac"] = round(fl / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[prec], 4)
+        rec = {"ms": round(ms, 4), "ms_source": "rocprof" if rp_ms else "bracketed", "bound": bound,
+               "mfma_floor_ms": round(f_mfma, 4), "hbm_floor_ms": round(f_hbm, 4)}
         if tb:
             rec["counted_bytes"] = tb
-            rec["counted_GBps"] = round(tb / (ms * 1e-3) / 1e9, 1)
-            rec["counted_hbm_frac"] = round(tb / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
             step_bytes += tb
-        alg = _alg_bytes_of(entry, M, prec, n_params)
-        if alg and tb:
-            rec["counted_over_algorithmic"] = round(tb / alg, 4)
+        if rp_ms:
+            af = (active or {}).get(M, 1.0) if entry != "nr_mlp_forward" else 1.0
+            fl = _flops_of(entry, M) * af
+            if fl:
+                rec["mfma_tflops"] = round(fl / (ms * 1e-3) / 1e12, 1)
+                rec["mfma_frac"] = round(fl / (ms * 1e-3) / 1e12 / PEAK_TFLOPS[prec], 4)
+                if af < 1.0:
+                    rec["active_tile_frac"] = round(af, 4)
+            if tb:
+                rec["counted_GBps"] = round(tb / (ms * 1e-3) / 1e9, 1)
+                rec["counted_hbm_frac"] = round(tb / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+            alg = _alg_bytes_of(entry, M, prec, n_params)
+            if alg and tb:
+                rec["counted_over_algorithmic"] = round(tb / alg, 4)
         out[key] = rec
     return out, step_bytes
 
 
-def headline_roofline(tflops: float, live_ms: float, rocprof_ms, prec: str):
-    """The dominant kernel on SURVEY §8d's MFMA basis: algorithmic FLOPs per launch over
-    its launch time -- the committed rocprof average of these sources when there is one
+def headline_roofline(tflops: float, live_ms: float, rocprof_ms, prec: str, active: float = 1.0):
+    """The dominant kernel on SURVEY §8d's MFMA basis: the algorithmic FLOPs of the work it
+    EXECUTED per launch (its active 32-sample tiles; all of them at bare init) over its
+    launch time -- the committed rocprof average of these sources when there is one
     (reproducible from profiles/), else the live HIP-event time."""
-    ach = tflops * live_ms / rocprof_ms if rocprof_ms else tflops
+    ach = (tflops * live_ms / rocprof_ms if rocprof_ms else tflops) * active
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[prec], "unit": "TFLOP/s",
             "frac": round(ach / PEAK_TFLOPS[prec], 4)}
 
@@ -354,8 +369,149 @@ def cpu_baseline(steps: int = 50, warmup: int = 5, context_steps: int = 3):
             "p10_p50_p90_rays_per_s": [round(c1["rays_per_s_p10"], 2), round(c1["rays_per_s_median"], 2),
                                        round(c1["rays_per_s_p90"], 2)],
             "cpu_model": _cpu_model(), "affinity_cpus": affinity, "threads": threads,
+            "threads_note": ("torch threads = min(len(sched_getaffinity), OMP_NUM_THREADS): the GPU box's affinity "
+                             "mask lists the whole machine's CPUs, but a one-GPU job's CPU share is "
+                             "OMP_NUM_THREADS (16) cores, so more threads would oversubscribe that share"
+                             if threads < affinity else "torch threads = len(sched_getaffinity)"),
             "context_64c128f_256rays": {"rays_per_s_median": round(c2["rays_per_s_median"], 2),
                                         "steps": context_steps, "seconds": round(c2["seconds"], 1)}}
+
+
+def active_tile_fracs(*nets):
+    """{M: mean fraction of the 32-sample tiles the backward ran on} from the counts the
+    networks recorded (NeRF._tile_counts, the kernels' own active-tile count), then stop
+    recording."""
+    acc = {}
+    for net in nets:
+        if net is None or net._tile_counts is None:
+            continue
+        for M, c in net._tile_counts:
+            a = acc.setdefault(M, [0, 0])
+            a[0] += int(c.item())
+            a[1] += (M + 31) // 32
+        net._tile_counts = None
+    return {M: a / t for M, (a, t) in acc.items() if t}
+
+
+# tests/psnr_parity.py's analytic scene: three soft-edged coloured spheres inside the lego
+# cameras' view, empty space elsewhere (white background)
+SPHERES = [((0.0, 0.0, 0.0), 0.7, (0.9, 0.2, 0.1)), ((0.8, 0.3, 0.2), 0.35, (0.1, 0.7, 0.2)),
+           ((-0.5, -0.6, 0.4), 0.45, (0.2, 0.3, 0.9))]
+
+
+def sphere_scene_field(pts):
+    sigma = torch.zeros(pts.shape[:-1], device=pts.device)
+    rgb = torch.ones(*pts.shape[:-1], 3, device=pts.device)
+    for c, r, col in SPHERES:
+        d = (pts - torch.tensor(c, device=pts.device)).norm(dim=-1)
+        sg = 40.0 * torch.sigmoid((r - d) * 40.0)
+        w = (sg / (sigma + sg + 1e-6))[..., None]
+        rgb = rgb * (1 - w) + torch.tensor(col, device=pts.device) * w
+        sigma = sigma + sg
+    return rgb, sigma
+
+
+def sphere_scene_rays(size: int, device):
+    """Every pixel ray of the 100 lego training cameras at size x size (views 0..89 train,
+    90..99 test) and the scene's ground truth, composited by the HIP kernels at 256
+    deterministic samples per ray."""
+    from noisy_src import ops
+    from noisy_src.rays import get_ray_directions, get_rays
+    fix = sorted((ROOT / "tests" / "golden").glob("final_poses_*.npz"))[0]
+    poses = torch.from_numpy(np.load(fix)["ground_truth_poses"]).float().to(device)
+    focal = 0.5 * size / math.tan(0.5 * 0.6911112070083618)
+    dirs = get_ray_directions(size, size, focal).to(device)
+    o, d = zip(*[get_rays(dirs, p) for p in poses])
+    o, d = torch.stack(o).reshape(-1, 3), torch.stack(d).reshape(-1, 3)
+    with torch.no_grad():
+        pts, z = ops.stratified_sample(o, d, 2.0, 6.0, 256)
+        rgb, sigma = sphere_scene_field(pts)
+        gt = ops.composite(rgb.contiguous(), sigma.contiguous(), z, d)[0]
+    return o, d, gt
+
+
+def train_sphere_state(precision: str, device, iters: int = 2000, size: int = 64, batch: int = 1024, seed: int = 0):
+    """A trained state: engine.Trainer on the sphere scene for ``iters``
+    iterations at ``batch`` rays from the seed-42 init.  Returns (trainer, (o, d, gt),
+    number of training rays)."""
+    from noisy_src.config import ModelConfig, RenderConfig
+    from noisy_src.engine import Trainer
+    from noisy_src.model import create_nerf
+    o, d, gt = sphere_scene_rays(size, device)
+    torch.manual_seed(42)
+    mc, mf = create_nerf(ModelConfig(precision=precision))
+    tr = Trainer(mc.to(device), mf.to(device), RenderConfig())
+    n_train = 90 * size * size
+    g = torch.Generator(device=device).manual_seed(seed)
+    for _ in range(iters):
+        idx = torch.randint(0, n_train, (batch,), device=device, generator=g)
+        tr.step(o[idx], d[idx], gt[idx])
+    torch.cuda.synchronize()
+    return tr, (o, d, gt), n_train
+
+
+def trained_state_leg(precision: str, device, B: int = 4096, steps: int = 50, iters: int = 2000):
+    """The same cfg #2 training step (64c+128f, B rays) on a TRAINED state, where the
+    backward skips the tiles with exactly zero incoming gradient (empty space: sigma == 0;
+    behind surfaces: transmittance underflowed to 0).  Same box, same state, alternating
+    skip / dense / skip runs of ``steps`` steps (the dense form is NrMlpConfig.dense_backward,
+    the reference's full backward): rays/s of each, the active-tile fraction the kernels
+    counted, and the fine dW launch on the executed work (HIP events, bracketed)."""
+    from noisy_src import _hip
+    t0 = time.perf_counter()
+    tr, (o, d, gt), n_train = train_sphere_state(precision, device, iters=iters)
+    train_s = time.perf_counter() - t0
+    g = torch.Generator(device=device).manual_seed(77)
+    pool = []
+    for _ in range(4):
+        idx = torch.randint(0, n_train, (B,), device=device, generator=g)
+        pool.append((o[idx].contiguous(), d[idx].contiguous(), gt[idx].contiguous()))
+    nets = (tr.model_coarse, tr.model_fine)
+    Mf = B * (tr.render_config.num_samples + tr.render_config.num_samples_fine)
+
+    def run(dense: bool):
+        for net in nets:
+            net._nr_cfg.dense_backward = int(dense)
+        for k in range(3):
+            tr.step(*pool[k % 4])
+        for net in nets:
+            net._tile_counts = []
+        timer = _hip.CallTimer(["nr_mlp_backward_dw", "nr_mlp_backward_dx"])
+        _hip.set_timer(timer)
+        for k in range(4):
+            tr.step(*pool[k % 4])
+        _hip.set_timer(None)
+        act = active_tile_fracs(*nets)
+        calls = timer.summary()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for k in range(steps):
+            tr.step(*pool[k % 4])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        dw = calls.get(f"nr_mlp_backward_dw[M={Mf}]", (0, float("nan")))[1]
+        dx = calls.get(f"nr_mlp_backward_dx[M={Mf}]", (0, float("nan")))[1]
+        af = act.get(Mf, 1.0)
+        return {"rays_per_s": round(B * steps / dt, 1), "ms_per_step": round(1e3 * dt / steps, 3),
+                "active_tile_frac": {str(k): round(v, 4) for k, v in sorted(act.items())},
+                "fine_dw_ms_bracketed": round(dw, 4), "fine_dx_ms_bracketed": round(dx, 4),
+                "fine_dw_executed_mfma_frac": round(2 * MACS_PER_EVAL * Mf * af / (dw * 1e-3) / 1e12
+                                                    / PEAK_TFLOPS[precision], 4)}
+
+    a1 = run(False)
+    dn = run(True)
+    a2 = run(False)
+    for net in nets:
+        net._nr_cfg.dense_backward = 0
+    skip_v = (a1["rays_per_s"] + a2["rays_per_s"]) / 2
+    return {"metric": "training rays/sec on a trained state (zero-gradient tiles skipped)",
+            "workload": f"sphere scene seen by the lego training cameras (64x64 views), {iters} iterations at "
+                        f"1024 rays from the seed-42 init ({train_s:.1f} s), then {B}-ray steps, "
+                        f"{tr.render_config.num_samples}c+{tr.render_config.num_samples_fine}f, {precision}",
+            "value": round(skip_v, 1), "unit": "rays/s",
+            "dense_value": dn["rays_per_s"], "skip_over_dense": round(skip_v / dn["rays_per_s"], 4),
+            "runs": {"skip_a": a1, "dense": dn, "skip_b": a2},
+            "note": "same box and state, alternating; the headline value stays the bare-init cfg #2 step"}
 
 
 def batch_assembly_ms(device, B: int, steps: int = 50):
@@ -486,6 +642,8 @@ def main():
                          "sliced over the ranks (default 0: weak scaling, --batch rays per GPU)")
     ap.add_argument("--cpu-steps", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-trained", action="store_true",
+                    help="skip the trained-state line (the step on a trained sphere-scene state, skip vs dense)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the training step as one captured hipGraph (engine.GraphedTrainer; with "
                          "data parallelism the RCCL all-reduces are captured too)")
@@ -561,10 +719,6 @@ def main():
         sl = slice(rank * B, (rank + 1) * B)
     else:
         B = args.batch
-    # engine.Trainer's rule for "auto": a graph replay of <= AUTO_COARSE_STREAM_RAYS rays
-    coarse_stream_used = not args.pose_opt and (
-        args.coarse_stream == "on" or (args.coarse_stream == "auto" and args.graph
-                                       and B <= Trainer.AUTO_COARSE_STREAM_RAYS))
     if args.pose_opt:
         # rays come from (image, pixel) and the learnable poses INSIDE the step; the
         # pixel draws (sampler.sample_batch) stay outside it, as batch sampling does below
@@ -596,8 +750,7 @@ def main():
     # every fused-MLP entry point is timed over the last warm-up steps (kernel_ms) to find
     # the dominant kernel; inside the timed region only that kernel's launches carry HIP
     # events (each bracketed call costs a few us of queue gap)
-    mlp_entries = ["nr_mlp_forward", "nr_mlp_backward_dx", "nr_mlp_backward_dw", "nr_mlp_backward_dxdw",
-                   "nr_mlp_backward_reduce"]
+    mlp_entries = ["nr_mlp_forward", "nr_mlp_backward_dx", "nr_mlp_backward_dw", "nr_mlp_backward_reduce"]
     wtimer = _hip.CallTimer(mlp_entries)
     # the data-parallel all-reduce is timed over the same warm-up steps (HIP events around
     # GradAllReducer's launch and wait), not inside the timed region: at small host-bound
@@ -608,9 +761,12 @@ def main():
             _hip.set_timer(wtimer)
             if reducer is not None:
                 reducer.timing = []
+            for net in (mc, mf):  # the backward's active-tile counts (work it executed)
+                net._tile_counts = []
         step(k)
     _hip.set_timer(None)
     torch.cuda.synchronize()
+    active = active_tile_fracs(mc, mf)
     ar_timing = reducer.timing_summary() if reducer is not None else None
     if reducer is not None:
         reducer.timing = None
@@ -673,15 +829,18 @@ def main():
     n_params = mf.flat_params().numel()
     bound, achieved, peak, unit, work = roofline_of(entry, M, ms, args.precision, n_params, dom_traffic)
     mf_tf, _, mf_work = mfma_roofline(entry, M, ms, args.precision)
+    dom_active = active.get(M, 1.0) if entry != "nr_mlp_forward" else 1.0
     if not mfma_macs_of(entry):
         # a dominant launch without MFMA work (e.g. the slab reduction): its byte roofline
         mf_tf, mf_work = None, work
+    elif dom_active < 1.0:
+        mf_work += f" x active-tile fraction {dom_active:.4f}"
     # the committed rocprofv3 kernel trace of this tree (same bench command): its average
-    # for the dominant kernel, and the fraction it gives (the live one is `frac`)
+    # for the dominant kernel, and the fraction it gives
     rp_rows, rp_src = rocprof_summary(args.precision)
     rp = next((rp_rows[(k, M)] for k in kern if (k, M) in rp_rows), None)
     rp_ms = float(rp.get("timed_avg_ms") or rp["avg_ms"]) if rp else None
-    ktab, step_bytes = kernel_table(wcalls, args.precision, n_params)
+    ktab, step_bytes = kernel_table(wcalls, args.precision, n_params, rp_rows, active)
     value = world * B * args.steps / dt
     out = {
         "metric": METRIC,
@@ -708,7 +867,8 @@ def main():
             "parallelism": f"dp{world}" + (" (RCCL process group, all-reduce in the step)" if pg is not None
                                            and world == 1 else ""),
             **({"execution": "hipGraph replay (engine.GraphedTrainer)"} if args.graph else {}),
-            **({"coarse_stream": "coarse chain on a second stream"} if coarse_stream_used else {}),
+            **({"coarse_stream": "coarse chain on a second stream"}
+               if getattr(trainer, "last_step_coarse_stream", False) else {}),
         },
         # headline: the dominant kernel on SURVEY §8d's MFMA basis (algorithmic FLOPs per
         # launch over its launch time); the stored-activation HBM view rides beside it
@@ -716,7 +876,7 @@ def main():
             # frac: from the committed rocprof kernel-trace average of these sources when
             # one exists (reproducible from profiles/), else from the live launch time;
             # MFMA basis, or the byte basis for a launch without MFMA work
-            **(headline_roofline(mf_tf, ms, rp_ms, args.precision) if mf_tf is not None else {
+            **(headline_roofline(mf_tf, ms, rp_ms, args.precision, dom_active) if mf_tf is not None else {
                 "bound": bound, "achieved": round(achieved * ms / rp_ms if rp_ms else achieved, 2), "peak": peak,
                 "unit": unit, "frac": round((achieved * ms / rp_ms if rp_ms else achieved) / peak, 4)}),
             "kernel": f"{kern[0]} via {entry} (M={M} samples, fine net)",
@@ -726,9 +886,13 @@ def main():
                            else "launch_ms: live HIP events on the launching stream over the timed region"),
             "traffic": dom_traffic,
             "work_per_launch": mf_work,
-            "launch_ms": round(ms, 4),
+            # the backward's executed share of the 32-sample tiles of this launch (tiles with
+            # a nonzero incoming gradient, counted by the kernels over the warm-up steps)
+            "active_tile_frac": round(dom_active, 4),
+            # HIP events around each launch over the timed region: carries queue gaps, so it
+            # is context only (no fraction is taken from it when a rocprof average exists)
+            "launch_ms_bracketed": round(ms, 4),
             "launches": n_launch,
-            "frac_live": round(mf_tf / PEAK_TFLOPS[args.precision], 4) if mf_tf is not None else None,
             "rocprof_ms": round(rp_ms, 4) if rp_ms else None,
             "rocprof_source": rp_src if rp_ms else None,
             "source_hash": source_hash(),
@@ -749,8 +913,13 @@ def main():
         "step_mfma_frac": round(value * 6 * MACS_PER_EVAL * (2 * rcfg.num_samples + rcfg.num_samples_fine)
                                 / (world * PEAK_TFLOPS[args.precision] * 1e12), 4),
         "step_ms_p10_p50_p90": step_pcts,
-        # per-launch means over the last warm-up steps (the roofline's launch_ms is live)
-        "kernel_ms": {k: round(v[1], 4) for k, v in wcalls.items()},
+        # per-launch ms of every fused-MLP key: the rocprof timed-region average where the
+        # committed same-source summary has it, else the bracketed warm-up mean (labelled)
+        "kernel_ms": {k: v["ms"] for k, v in ktab.items()},
+        "kernel_ms_source": sorted({v["ms_source"] for v in ktab.values()}),
+        # each key launches once per step: the fused-MLP launches' share of ms_per_step
+        "kernel_ms_sum": round(sum(v["ms"] for v in ktab.values()), 4),
+        "active_tile_frac": {str(k): round(v, 4) for k, v in sorted(active.items())},
         "final_loss": round(loss, 6),
         # the lego test split is not available offline: the PSNR half of the
         # metric is the recorded equal-iteration comparison on the analytic scene
@@ -760,6 +929,9 @@ def main():
         out["topology"] = topology
     if rank == 0 and world == 1:
         out["batch_assembly_ms_per_step"] = batch_assembly_ms(dev, B)
+    if (rank == 0 and world == 1 and not args.pose_opt and not args.graph and not strong and not args.no_trained
+            and (rcfg.num_samples, rcfg.num_samples_fine) == (64, 128)):
+        out["trained_state"] = trained_state_leg(args.precision, dev, B=B)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.pose_opt:
         out["cpu_baseline"] = cpu_baseline(steps=args.cpu_steps)
     if rank == 0:

@@ -184,6 +184,9 @@ typedef struct NrMlpConfig {
     uint32_t skip_mask; /* bit i set <=> i in ModelConfig.skips */
     int use_view_dirs;  /* ModelConfig.use_view_dirs (1)       */
     int precision;      /* NR_PREC_FP32 / NR_PREC_BF16         */
+    int dense_backward; /* 0: the backward skips 32-sample tiles whose incoming
+                           gradient (g_rgb, g_sigma) is exactly zero; nonzero:
+                           every tile (the dense reference form)          */
 } NrMlpConfig;
 
 #define NR_PREC_FP32 0
@@ -220,9 +223,15 @@ int nr_mlp_backward(const NrMlpConfig* cfg, const void* packed,
                     float* g_d, void* workspace, nr_stream_t stream);
 
 /* The three stages of nr_mlp_backward, callable separately (per-kernel timing):
- * dx: dz of every layer into the workspace (+ g_x / g_d); dw: per-chunk dW/db
- * slabs from the saved activations and dz; reduce: slabs -> g_params (chunk
- * order, deterministic).  Same arguments and workspace as nr_mlp_backward. */
+ * dx: the list of ACTIVE 32-sample tiles (any nonzero g_rgb / g_sigma entry;
+ * every tile with cfg->dense_backward) and the dz of every layer for them into
+ * the workspace (+ g_x / g_d, zero for inactive samples); dw: per-chunk dW/db
+ * slabs from the saved activations and dz of the active tiles, split over the
+ * chunks in list order; reduce: slabs -> g_params (chunk order, deterministic).
+ * A tile whose incoming gradient is exactly zero has dz == 0 in every layer, so
+ * skipping it drops only exact-zero terms; when every tile is active the result
+ * is bit-identical to the dense form.  Same arguments and workspace as
+ * nr_mlp_backward; dw must follow dx on the same workspace.                 */
 int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed,
                        const float* params, const float* x, const float* d,
                        int64_t M, const float* rgb, const float* sigma,
@@ -234,27 +243,9 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved,
 int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M,
                            const void* workspace, float* g_params,
                            nr_stream_t stream);
-/* dx + dw as ONE layer-pipelined launch (16-bit): one workgroup per layer and
- * sample range, dz handed between layers through on-chip-resident rings in the
- * workspace instead of HBM images; writes the same per-chunk slabs (bit-identical
- * to dx then dw), so nr_mlp_backward_reduce follows it.  g_x / g_d as
- * nr_mlp_backward_dx.  Outside its envelope (fp32, more than one skip layer,
- * fewer CUs than pipelines x stages) it runs dx then dw itself.              */
-int nr_mlp_backward_dxdw(const NrMlpConfig* cfg, const void* packed,
-                         const float* params, const float* x, const float* d,
-                         int64_t M, const float* rgb, const float* sigma,
-                         const void* saved, const float* g_rgb,
-                         const float* g_sigma, float* g_x, float* g_d,
-                         void* workspace, nr_stream_t stream);
-/* 1 if nr_mlp_backward_dxdw runs the pipelined kernel for (cfg, M) on the
- * current device, else 0.                                                   */
-int nr_mlp_backward_pipelined(const NrMlpConfig* cfg, int64_t M);
-/* Byte offset in the workspace of the pipelined backward's status word (0 = ok,
- * nonzero = a bounded wait timed out), or -1.  A stage that finds the word set
- * when it ends writes NaN into its dW slabs, so nr_mlp_backward_reduce then
- * yields NaN gradients (a loud failure: the clip norm and every Adam update
- * turn NaN) instead of silently wrong ones.                                   */
-int64_t nr_mlp_pipe_status_offset(const NrMlpConfig* cfg, int64_t M);
+/* Byte offset in the workspace of the uint32 count of active tiles that
+ * nr_mlp_backward_dx wrote (of ceil(M / 32)), or -1: the work the backward ran. */
+int64_t nr_mlp_active_tiles_offset(const NrMlpConfig* cfg, int64_t M);
 
 /* ---- A13: optimizer tail  (noisy_src/train.py:112-117, train_pose_opt.py:398-409)
  * Sum of squares of n fp32 values added into *acc (device scalar, caller-zeroed):

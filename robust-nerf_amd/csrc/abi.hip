@@ -27,7 +27,7 @@ extern "C" {
 
 const char* nr_last_error(void) { return nr::g_last_error; }
 
-int nr_abi_version(void) { return 4; }
+int nr_abi_version(void) { return 5; }
 
 int nr_probe_fill(float* out, int n, float value, nr_stream_t stream) {
     NR_REQUIRE(out != nullptr && n >= 0, "nr_probe_fill: bad arguments");

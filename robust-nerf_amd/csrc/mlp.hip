@@ -28,21 +28,6 @@
 #include <type_traits>
 #include <utility>
 
-// Timing-only A/B switches that compute WRONG results (dropped stores, a racing LDS
-// ring, skipped DMA/barriers/MFMAs/bias sums) exist for tools/build_variant.sh, which
-// builds them into noisy_src/lib/variants/ with NR_AB_VARIANT defined.  The product
-// library (Makefile) refuses every one of them, so a stray -D cannot ship.
-#if !defined(NR_AB_VARIANT)
-#if defined(NR_NOSTORE_IMG) || defined(NR_RBM_NOWAIT) || (defined(NR_DW_NOCOMPUTE) && NR_DW_NOCOMPUTE) || \
-    (defined(NR_DW_NOBIAS) && NR_DW_NOBIAS) || (defined(NR_AB_NODMA) && NR_AB_NODMA) ||                   \
-    (defined(NR_AB_NOBAR) && NR_AB_NOBAR) || (defined(NR_AB_NOWAIT) && NR_AB_NOWAIT) ||                   \
-    (defined(NR_AB_HALFA) && NR_AB_HALFA) || (defined(NR_FWD_NOSINK) && NR_FWD_NOSINK) || defined(NR_PIPE_ONLY) || \
-    (defined(NR_AB_PIPE_NORING) && NR_AB_PIPE_NORING) || (defined(NR_AB_PIPE_NOSTAGE) && NR_AB_PIPE_NOSTAGE) || \
-    (defined(NR_AB_PIPE_NOWAIT) && NR_AB_PIPE_NOWAIT)
-#error "wrong-result A/B switch in a product build: build it with tools/build_variant.sh (NR_AB_VARIANT)"
-#endif
-#endif
-
 #include "common.hpp"
 #include "mfma.hpp"
 #include "mlp_plan.hpp"
@@ -198,23 +183,8 @@ __device__ __forceinline__ void pe_feat_bwd(float x0, float x1, float x2, int f,
 #ifndef NR_APF
 #define NR_APF 3  // 16-bit weight-stream A fragments read ahead (row blocks)
 #endif
-#ifndef NR_AB_NOWAIT
-#define NR_AB_NOWAIT 0
-#endif
-#ifndef NR_AB_HALFA
-#define NR_AB_HALFA 0
-#endif
-#ifndef NR_AB_NODMA
-#define NR_AB_NODMA 0  // A/B timing only (wrong results): no weight-stream DMA
-#endif
-#ifndef NR_AB_NOBAR
-#define NR_AB_NOBAR 0  // A/B timing only (racy): no stream barrier
-#endif
 #ifndef NR_NT_STORE
 #define NR_NT_STORE 1
-#endif
-#ifndef NR_FWD_NOSINK
-#define NR_FWD_NOSINK 0  // A/B only: skip the saved-activation stores of the training forward
 #endif
 #ifndef NR_FASTPE
 #define NR_FASTPE 1
@@ -403,9 +373,7 @@ __device__ __forceinline__ void store_img(char* __restrict__ region, int64_t til
     // wave-uniform base (tile is per wave) + the lane's 16 B: saddr + voffset stores
     char* base = region + ((tile * nblk + blk) * kFPB<PREC>) * static_cast<int64_t>(kFragBytes) + lane16();
     if constexpr (k16<PREC>) {
-#if defined(NR_NOSTORE_IMG)  // A/B only: keep the values, drop the stores (wrong results)
-        asm volatile("" ::"v"(v.s[0]), "v"(v.s[1]), "v"(base));
-#elif NR_NT_STORE
+#if NR_NT_STORE
         // streaming (non-temporal) stores: the 4 GB of images must not evict the
         // L2-resident weight stream every workgroup re-reads
         __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v.s[0]), reinterpret_cast<u32x4*>(base));
@@ -566,7 +534,6 @@ struct Stager {
     }
     // chunk q of ckb KB (advance cadv KB): sizes from the caller, no scalar loads
     __device__ __forceinline__ void load_sized(Ring& ring, int q, int ckb, int cadv, int) {
-        if (NR_AB_NODMA) return;
         const int bytes = ckb * 1024;
         char* slot = ring.lds + (q & 1) * ring.slot_bytes;
         const uint32_t l16 = lane16();
@@ -581,7 +548,6 @@ struct Stager {
     // ops issued since (the chunk's saved-activation / dz stores) may stay in flight
     // across the barrier (vmcnt retires in issue order).
     __device__ __forceinline__ void store(char*, const StreamDesc&, int, int, int after = 0) {
-        if (NR_AB_NOWAIT) return;  // A/B timing only (racy)
         switch (after) {
             case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
             case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
@@ -678,7 +644,7 @@ struct Sink {
 // stager's counted vmcnt.
 __device__ __forceinline__ void stream_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!NR_AB_NOBAR) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
 
@@ -686,11 +652,7 @@ __device__ __forceinline__ void stream_barrier() {
 // see stream_gemm) and the counted wait that publishes them.
 __device__ __forceinline__ void ds_read_pair(bf16x8 (&dst)[2], uint32_t addr) {
     asm volatile("ds_read_b128 %0, %1" : "=v"(dst[0]) : "v"(addr));
-#if NR_AB_HALFA  // A/B timing only (wrong results): half the LDS read traffic
-    dst[1] = dst[0];
-#else
     asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(dst[1]) : "v"(addr));
-#endif
 }
 // wait until at most n LDS/SMEM ops are outstanding (n: the reads issued after
 // these two, all younger LDS reads; SMEM only ever makes this wait longer)
@@ -948,7 +910,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     for (int t = 0; t < TPW; ++t) tokm |= (tok[t] ? 1u : 0u) << t;
     // training saves each layer input as the next stream consumes it
     auto sink_of = [&](int sv, int nblk) {
-        return Sink<PREC, TPW>{(TRAIN && !NR_FWD_NOSINK) ? a.saved + a.sv_off[sv] : nullptr, nblk, tile0, tokm};
+        return Sink<PREC, TPW>{TRAIN ? a.saved + a.sv_off[sv] : nullptr, nblk, tile0, tokm};
     };
 
     Ring ring{lds, a.slot_bytes, 0, nullptr, wv};
@@ -1246,6 +1208,8 @@ struct BwdArgs {
     const char* saved;
     char* ws;
     int64_t M, tiles;
+    const uint32_t* list;  // active tiles (tile_list_kernel) and their count
+    const uint32_t* count;
     int L, Ld, n_layers;
     uint32_t skips;
     int slot_bytes;
@@ -1262,14 +1226,20 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ml = lane & 31;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t tile0 = (static_cast<int64_t>(blockIdx.x) * (NT / 64) + wv) * TPW;
+    // wave -> entry blockIdx.x * (NT / 64) + wv of the active-tile list (one tile per wave);
+    // waves past its end run on zero inputs and store nothing
+    static_assert(TPW == 1, "the active-tile list gives each wave one tile");
+    const int64_t cnt = *a.count;
+    const int64_t slot = static_cast<int64_t>(blockIdx.x) * (NT / 64) + wv;
+    if (static_cast<int64_t>(blockIdx.x) * (NT / 64) >= cnt) return;
+    const int64_t tile0 = slot < cnt ? static_cast<int64_t>(a.list[slot]) : 0;
     const int n = a.n_layers;
     const u32x4* masks = reinterpret_cast<const u32x4*>(a.saved + a.mask_off);
     bool tok[TPW];
     unsigned tokm = 0u;
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        tok[t] = tile0 + t < a.tiles;
+        tok[t] = slot + t < cnt;
         tokm |= (tok[t] ? 1u : 0u) << t;
     }
     // each dz image is saved while the next stream consumes it
@@ -1297,7 +1267,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
         const int64_t m = (tile0 + t) * 32 + ml;
-        const bool valid = m < a.M;
+        const bool valid = tok[t] && m < a.M;
         float dr[3] = {0.f, 0.f, 0.f};
         dzs[t] = 0.f;
         if (valid) {
@@ -1366,7 +1336,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
 #pragma unroll
             for (int t = 0; t < TPW; ++t) {
                 const int64_t m = (tile0 + t) * 32 + ml;
-                const bool valid = m < a.M;
+                const bool valid = tok[t] && m < a.M;
                 const float d0 = valid ? a.d[3 * m] : 0.f, d1 = valid ? a.d[3 * m + 1] : 0.f,
                             d2 = valid ? a.d[3 * m + 2] : 0.f;
                 float g0 = 0.f, g1 = 0.f, g2 = 0.f;
@@ -1480,7 +1450,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
 #pragma unroll
             for (int t = 0; t < TPW; ++t) {
                 const int64_t m = (tile0 + t) * 32 + ml;
-                const bool valid = m < a.M;
+                const bool valid = tok[t] && m < a.M;
                 const float x0 = valid ? a.x[3 * m] : 0.f, x1 = valid ? a.x[3 * m + 1] : 0.f,
                             x2 = valid ? a.x[3 * m + 2] : 0.f;
                 float g0 = 0.f, g1 = 0.f, g2 = 0.f;
@@ -1522,6 +1492,7 @@ struct DinArgs {
     float* g_x;
     float* g_d;
     int64_t M, tiles;
+    const uint8_t* flags;         // active tiles (tile_flags_kernel): the others have dz == 0
     int L, Ld;
     float inv_gscale;
     int nsrc;                     // x_enc-reading layers
@@ -1577,6 +1548,17 @@ __global__ __launch_bounds__(kDinNT) void mlp_dinput_kernel(DinArgs a) {
         const int64_t tile_u = __builtin_amdgcn_readfirstlane(static_cast<int>(tile));
         const int64_t m = tile * 32 + ml;
         const bool valid = m < a.M;
+        if (!a.flags[tile_u]) {
+            // no incoming gradient in this tile: its dz were never computed, and its input
+            // gradients are exactly zero
+            if (valid && h == 0)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    if (a.g_x) a.g_x[3 * m + c] = 0.f;
+                    if (a.g_d) a.g_d[3 * m + c] = 0.f;
+                }
+            continue;
+        }
         if (a.g_x) {
             f32x16 dxe[XB];
 #pragma unroll
@@ -1650,6 +1632,78 @@ __global__ __launch_bounds__(kDinNT) void mlp_dinput_kernel(DinArgs a) {
     }
 }
 
+// ----------------------------------------------------- active tiles ----
+// The backward's work list.  A sample whose sigma is exactly 0 (alpha = w = 0, and
+// ReLU'(0) = 0 on sigma: reference rendering.py:83) or whose transmittance has
+// underflowed to 0 (the cumprod of 1 - alpha + 1e-10, rendering.py:87-96) receives
+// exactly zero g_rgb and g_sigma, so every layer's dz for it is zero.  A 32-sample
+// tile of such samples only adds exact zeros to dW, so the dX chain, the dW GEMM and
+// the input gradients run over the tiles with ANY nonzero incoming gradient.  The flag
+// is computed from the values (never assumed), in two launches: per-tile flags, then
+// one workgroup compacts them in tile order (deterministic list).
+constexpr int kTileFlagThreads = 256;  // 4 waves x 16 tiles per workgroup
+constexpr int kTilesPerFlagWg = 64;
+constexpr int kTileListThreads = 1024;
+
+__global__ __launch_bounds__(kTileFlagThreads) void tile_flags_kernel(const float* __restrict__ g_rgb,
+                                                                      const float* __restrict__ g_sigma, int64_t M,
+                                                                      int64_t tiles, int dense,
+                                                                      uint8_t* __restrict__ flags) {
+    const int lane = threadIdx.x & 63;
+    const int64_t tw = static_cast<int64_t>(blockIdx.x) * kTilesPerFlagWg + (threadIdx.x >> 6) * 16;
+    bool nz[8];
+    // lanes 0-31: tile tw + 2 it, lanes 32-63: tile tw + 2 it + 1 (one sample each)
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int64_t m = (tw + 2 * it + (lane >> 5)) * 32 + (lane & 31);
+        bool v = false;
+        if (m < M) {
+            if (dense) {
+                v = true;
+            } else {
+                const float r0 = g_rgb[3 * m], r1 = g_rgb[3 * m + 1], r2 = g_rgb[3 * m + 2], s0 = g_sigma[m];
+                v = (r0 != 0.f) | (r1 != 0.f) | (r2 != 0.f) | (s0 != 0.f);  // NaN counts as nonzero
+            }
+        }
+        nz[it] = v;
+    }
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const uint64_t b = __ballot(nz[it]);
+        const int64_t t = tw + 2 * it + (lane >> 5);
+        if ((lane & 31) == 0 && t < tiles)
+            flags[t] = static_cast<uint8_t>(((lane >> 5) ? (b >> 32) : (b & 0xffffffffull)) != 0);
+    }
+}
+
+// flags -> list of the active tiles in increasing order, and their count: thread i
+// counts its contiguous share of the flags, a workgroup scan gives its first slot.
+__global__ __launch_bounds__(kTileListThreads) void tile_list_kernel(const uint8_t* __restrict__ flags,
+                                                                     int64_t tiles, uint32_t* __restrict__ list,
+                                                                     uint32_t* __restrict__ count) {
+    __shared__ uint32_t part[kTileListThreads];
+    const int i = threadIdx.x;
+    const int64_t per = (tiles + kTileListThreads - 1) / kTileListThreads;
+    int64_t lo = i * per;
+    if (lo > tiles) lo = tiles;
+    int64_t hi = lo + per;
+    if (hi > tiles) hi = tiles;
+    uint32_t c = 0;
+    for (int64_t t = lo; t < hi; ++t) c += flags[t];
+    part[i] = c;
+    __syncthreads();
+    for (int off = 1; off < kTileListThreads; off <<= 1) {  // inclusive scan (Hillis-Steele)
+        const uint32_t v = i >= off ? part[i - off] : 0u;
+        __syncthreads();
+        part[i] += v;
+        __syncthreads();
+    }
+    uint32_t slot = part[i] - c;
+    for (int64_t t = lo; t < hi; ++t)
+        if (flags[t]) list[slot++] = static_cast<uint32_t>(t);
+    if (i == kTileListThreads - 1) *count = part[i];
+}
+
 // ------------------------------------------------------------------ dW ----
 // Workgroup = (job, chunk of tiles): 8 waves, each accumulating its planned share
 // (DwWave: up to 5x2 blocks) of the job's NBz x KB output grid.  Per tile the
@@ -1658,8 +1712,8 @@ __global__ __launch_bounds__(kDinNT) void mlp_dinput_kernel(DinArgs a) {
 // 1-KB wave pieces) and the sample-major MFMA operands are rebuilt from the
 // B-operand images.  Bias partials are v_dot2 sums of the dz operands.  Output
 // slab per chunk: [dz row][input col | bias] fp32.  The kernel runs at its staging
-// ceiling: the same staging with the MFMAs compiled out (NR_DW_NOCOMPUTE) is
-// within 1 % of it.
+// ceiling: the same staging with the MFMAs compiled out (a timing-only variant,
+// r02) is within 1 % of it.
 #ifndef NR_DW_NSTAGE
 #define NR_DW_NSTAGE 4  // LDS staging ring depth of the dW kernel (tiles)
 #endif
@@ -1668,12 +1722,6 @@ __global__ __launch_bounds__(kDinNT) void mlp_dinput_kernel(DinArgs a) {
 #endif
 #ifndef NR_DW_ONESHAPE
 #define NR_DW_ONESHAPE 0  // A/B only: every 16-bit wave share runs as 5x2
-#endif
-#ifndef NR_DW_NOBIAS
-#define NR_DW_NOBIAS 0  // A/B only: skip the bias sums (wrong bias gradients)
-#endif
-#ifndef NR_DW_NOCOMPUTE
-#define NR_DW_NOCOMPUTE 0  // A/B only: stage the tiles, skip the MFMAs (staging ceiling)
 #endif
 constexpr int kDwThreads = 512;
 constexpr int kDwWaves = kDwThreads / 64;
@@ -1684,7 +1732,9 @@ struct DwArgs {
     float* slabs;
     int njobs;
     int64_t tiles;
-    int job_tpc[kMaxJobs];          // tiles per chunk of each job
+    const uint32_t* list;           // active tiles (tile_list_kernel) and their count
+    const uint32_t* count;
+    int job_chunks[kMaxJobs];       // chunks of each job: list entries split evenly in order
     uint16_t wg_map[kDwMaxWgs];     // workgroup -> job | chunk << 5 (chunk-major: one chunk of every job in a row)
     int stage_bytes, nstage;
     int64_t slab_floats_per_chunk;
@@ -1781,9 +1831,13 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     const int row0 = winfo & 63, np = (winfo >> 6) & 7, col0 = (winfo >> 9) & 63, nq = (winfo >> 15) & 3;
     const bool active = np > 0;
     const bool do_bias = active && ((winfo >> 17) & 1);
-    const int64_t t0 = static_cast<int64_t>(chunk) * a.job_tpc[j];
-    int64_t t1 = t0 + a.job_tpc[j];
-    if (t1 > a.tiles) t1 = a.tiles;
+    // this chunk's entries [t0, t1) of the active-tile list: ceil(count / chunks) each, in
+    // list order (with every tile active, exactly the dense form's contiguous ranges)
+    const int64_t cnt = *a.count;
+    const int64_t tpc = (cnt + a.job_chunks[j] - 1) / a.job_chunks[j];
+    const int64_t t0 = static_cast<int64_t>(chunk) * tpc;
+    int64_t t1 = t0 + tpc;
+    if (t1 > cnt) t1 = cnt;
     constexpr int FPB = kFPB<PREC>;
     constexpr int BLK = FPB * kFragBytes;
 
@@ -1797,7 +1851,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     const int total = (NBz + KB) * FPB;
     const int per_wave = (total + kDwWaves - 1) / kDwWaves;
     constexpr int kMaxPW = dw_max_pieces(k16<PREC>);  // the plan keeps per_wave <= kMaxPW
-    const char* psrc[kMaxPW];
+    const char* psrc[kMaxPW];  // piece k of tile 0 (lane's 16 B); tile t adds t * pstride[k]
     int64_t pstride[kMaxPW];
     int pdst[kMaxPW];  // LDS offset within a stage, or -1: scratch KB
 #pragma unroll
@@ -1814,21 +1868,22 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
             const int nb = a.seg_blocks[j][sg];
             const int L = k16<PREC> ? dw_slot(lane, (pc - p0) % FPB) : dw_slot32(lane, (pc - p0) % FPB);
             pstride[k] = static_cast<int64_t>(nb) * BLK;
-            psrc[k] = a.seg_ptr[j][sg] + t0 * pstride[k] + (pc - p0) * kFragBytes + L * 16;
+            psrc[k] = a.seg_ptr[j][sg] + (pc - p0) * kFragBytes + L * 16;
             pdst[k] = pad ? -1 : pc * kFragBytes;
         }
     }
-    // stages are issued in tile order, so each piece's source pointer just advances
-    auto stage = [&](int b) {
+    // stage list entry `pos` (tile list[pos], a scalar load) into buffer b
+    auto stage = [&](int b, int64_t pos) {
         char* dst = lds + b * a.stage_bytes;
         char* scratch = lds + a.nstage * a.stage_bytes;
+        const int64_t tile = a.list[pos];
 #pragma unroll
         for (int k = 0; k < kMaxPW; ++k) {
             if (k < per_wave) {
                 char* d = pdst[k] < 0 ? scratch : dst + pdst[k];
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(psrc[k]),
-                                                 (__attribute__((address_space(3))) void*)(d), 16, 0, NR_DW_AUX);
-                psrc[k] += pstride[k];
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(psrc[k] + tile * pstride[k]),
+                    (__attribute__((address_space(3))) void*)(d), 16, 0, NR_DW_AUX);
             }
         }
     };
@@ -1875,7 +1930,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
         for (int q = 0; q < NQ; ++q) kval[q] = q < nq;
 
         for (int k = 0; k < NS - 1; ++k)
-            if (t0 + k < t1) stage(k);
+            if (t0 + k < t1) stage(k, t0 + k);
         int bcur = 0, bnext = NS - 1;  // stage of tile t, stage tile t+NS-1 goes to
         for (int64_t t = t0; t < t1; ++t) {
             // stages t+1 .. t+NS-2 may stay in flight
@@ -1884,11 +1939,11 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
             wait_pieces(per_wave * static_cast<int>(ahead));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
-            if (t + NS - 1 < t1) stage(bnext);
+            if (t + NS - 1 < t1) stage(bnext, t + NS - 1);
             bnext = bnext + 1 == NS ? 0 : bnext + 1;
             const char* buf = lds + bcur * a.stage_bytes;
             bcur = bcur + 1 == NS ? 0 : bcur + 1;
-            if (NR_DW_NOCOMPUTE || !active) continue;
+            if (!active) continue;
             if constexpr (k16<PREC>) {
                 const uint32_t base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(buf));
                 const uint32_t bufA = base + row0 * BLK, bufB = base + (NBz + col0) * BLK;
@@ -1924,7 +1979,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
 #pragma unroll
                         for (int q = 0; q < NQ; ++q) acc[p][q] = mfma16<PREC>(A[p], Bm[q], acc[p][q]);
                     // bias gradient = dz summed over samples: lane-local fp32 partials
-                    if (do_bias && !NR_DW_NOBIAS)
+                    if (do_bias)
 #pragma unroll
                         for (int p = 0; p < NP; ++p) bsum[p] = dw_acc4<PREC>(ra[p][1], dw_acc4<PREC>(ra[p][0], bsum[p]));
                 }
@@ -2353,8 +2408,6 @@ __global__ void __launch_bounds__(kSumsqThreads) adam_multi_kernel(AdamMultiArgs
     }
 }
 
-#include "mlp_pipe.inc"
-
 }  // namespace nr
 
 using namespace nr;
@@ -2535,6 +2588,7 @@ int input_grads16(const MlpPlan& p, const MlpSizes& z, const char* packed, const
     std::memset(&da, 0, sizeof(da));
     da.packed = packed;
     da.ws = ws;
+    da.flags = reinterpret_cast<const uint8_t*>(ws + z.flags_off);
     da.x = x;
     da.d = d;
     da.g_x = g_x;
@@ -2562,143 +2616,6 @@ int input_grads16(const MlpPlan& p, const MlpSizes& z, const char* packed, const
     return p.prec == NR_PREC_BF16 ? launch_dinput<NR_PREC_BF16>(p, da, s) : launch_dinput<NR_PREC_FP16>(p, da, s);
 }
 
-// ---- fused layer-pipelined backward (mlp_pipe.inc) ----
-// The stage layout of a plan, or false when the plan is not one the pipeline covers:
-// 16-bit, exactly one x-job (layer 0 and at most one skip layer) and the split plan's
-// job order (x, h-jobs 1..n-1, feat, dir), whose slabs the stages write.
-bool pipe_layout(const MlpPlan& p, const MlpSizes& z, PipeArgs& a, int& NX) {
-    if (p.fpb != 2 || z.pipe_edges != p.n_layers + 1) return false;
-    const int n = p.n_layers;
-    if (p.n_jobs != n + 2 || n + 2 > kPipeMaxStages) return false;
-    const DwJob& xj = p.job[0];
-    NX = xj.ndz;
-    if (NX < 1 || NX > 2 || xj.nin != 1 || xj.in[0].is_ws || xj.in[0].tensor != SV_XENC) return false;
-    int xl[2] = {-1, -1};
-    for (int x = 0; x < NX; ++x) {
-        if (!xj.dz[x].is_ws) return false;
-        xl[x] = xj.dz[x].tensor - WS_DZ0;
-    }
-    if (xl[0] != 0 || (NX == 2 && (xl[1] < 1 || xl[1] >= n))) return false;
-    // S_X reads the skip layer's dz and dz_0, which the chain of trunk stages delivers ~4
-    // tiles per hop later (mlp_pipe.inc, the schedule): the skip layer's producer runs that
-    // far ahead of S_X's frees, so its ring must hold the lag
-    if (NX == 2 && 4 * xl[1] + 8 > kPipeRingSlots) return false;
-    for (int i = 1; i < n; ++i) {
-        const DwJob& j = p.job[i];
-        if (j.ndz != 1 || j.nin != 1 || !j.dz[0].is_ws || j.dz[0].tensor != WS_DZ0 + i || j.in[0].is_ws ||
-            j.in[0].tensor != SV_H0 + i - 1)
-            return false;
-    }
-    const int jfeat = n, jdir = n + 1;
-    if (p.job[jfeat].dz[0].tensor != p.ws_feat || p.job[jdir].dz[0].tensor != p.ws_dir || p.job[jfeat].NBz != kHB + 1)
-        return false;
-    auto x_of = [&](int layer) { return layer == xl[0] ? 0 : (NX == 2 && layer == xl[1] ? 1 : -1); };
-    // edge j carries dz_j (j < n) or dz_feat (j = n); an x-layer j >= 1 has S_X as its second consumer
-    auto ncons = [&](int j) { return (j >= 1 && x_of(j) >= 0) ? 2 : 1; };
-    a.nstage = n + 2;
-    a.nedge = n + 1;
-    for (int s = 0; s < a.nstage; ++s) {
-        PipeStageDesc& st = a.st[s];
-        std::memset(&st, 0, sizeof(st));
-        st.in_edge = st.out_edge = -1;
-        if (s == 0) {
-            st.kind = PK_DIR;
-            st.out_edge = n;
-            st.out_ncons = 1;
-            st.job = jdir;
-            st.mask_layer = n;
-            st.w_img = p.lin[n + 1].pk_bwdr;
-            st.ws_store[0] = z.ws_off[p.ws_dir];
-        } else if (s == 1) {
-            st.kind = PK_FEAT;
-            st.in_edge = n;
-            st.out_edge = n - 1;
-            st.out_ncons = ncons(n - 1);
-            st.job = jfeat;
-            st.mask_layer = n - 1;
-            st.w_img = p.lin[n].pk_bwdr;
-            st.sv_in = z.saved_off[SV_H0 + n - 1];
-        } else if (s <= n) {
-            const int i = n + 1 - s;
-            st.kind = PK_TRUNK;
-            st.in_edge = i;
-            st.out_edge = i - 1;
-            st.out_ncons = ncons(i - 1);
-            st.job = i;
-            st.mask_layer = i - 1;
-            st.w_img = p.lin[i].pk_bwdr;
-            st.sv_in = z.saved_off[SV_H0 + i - 1];
-        } else {
-            st.kind = PK_X;
-            for (int x = 0; x < NX; ++x) {
-                st.x_edge[x] = xl[x];
-                st.x_cons[x] = xl[x] >= 1 ? 1 : 0;
-                st.ws_store[x] = z.ws_off[WS_DZ0 + xl[x]];
-            }
-            st.job = 0;
-            st.job2 = jfeat;
-            st.sv_in = z.saved_off[SV_XENC];
-        }
-    }
-    for (int j = 0; j < p.n_jobs; ++j) {
-        a.job_slab[j] = p.job[j].slab_off;
-        a.job_ld[j] = p.job[j].KB * 32 + 1;
-    }
-    return true;
-}
-
-// CUs of the current device (the pipeline needs every workgroup resident at once)
-int device_cus() {
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    if (cus[dev] == 0) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-        cus[dev] = v;
-    }
-    return cus[dev];
-}
-
-template <int PREC, int XB, int DB, int NX>
-bool pipe_resident_one_per_cu() {
-    static int ok = -1;  // one query per instantiation
-    if (ok < 0) {
-        int nb = 0;
-        const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &nb, reinterpret_cast<const void*>(&mlp_bwd_pipe_kernel<PREC, XB, DB, NX>), kPipeThreads,
-            pipe_lds_bytes(XB, DB, NX));
-        ok = (e == hipSuccess && nb >= 1) ? 1 : 0;
-    }
-    return ok == 1;
-}
-
-// One compiled instance per (XB, DB, NX): the reference's encodings (pos_freqs 10:
-// XB 2), with / without view dirs and skip; other encodings run the split backward.
-// LAUNCH false: only report whether the instance exists and is resident one per CU
-// (nr_mlp_backward_pipelined), true: launch it.
-template <int PREC>
-int launch_pipe(const MlpPlan& p, const PipeArgs& a, int NX, hipStream_t s, bool* launched, bool launch = true) {
-    *launched = false;
-    const dim3 grid(static_cast<unsigned>(a.npipe * a.nstage)), block(kPipeThreads);
-#define NR_PIPE(XB_, DB_, NX_)                                                                               \
-    if (p.XB == XB_ && p.DB == DB_ && NX == NX_) {                                                           \
-        if (!pipe_resident_one_per_cu<PREC, XB_, DB_, NX_>()) return NR_OK;                                  \
-        *launched = true;                                                                                    \
-        if (!launch) return NR_OK;                                                                           \
-        hipLaunchKernelGGL((mlp_bwd_pipe_kernel<PREC, XB_, DB_, NX_>), grid, block, pipe_lds_bytes(XB_, DB_, NX_), \
-                           s, a);                                                                            \
-        return check_launch("nr_mlp_backward_dxdw");                                                         \
-    }
-    NR_PIPE(2, 1, 2)
-#ifndef NR_MLP_DEV
-    NR_PIPE(2, 1, 1)
-    NR_PIPE(2, 0, 2)
-    NR_PIPE(2, 0, 1)
-#endif
-#undef NR_PIPE
-    return NR_OK;  // no instance: the caller runs the split backward
-}
 
 }  // namespace
 
@@ -2985,6 +2902,17 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     if (M == 0) return NR_OK;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const MlpSizes z = make_sizes(p, M);
+    NR_REQUIRE(z.tiles_alloc < (int64_t{1} << 32), "nr_mlp_backward_dx: M beyond 2^37 samples");
+    // the active-tile list (every tile with cfg->dense_backward)
+    char* wsb = static_cast<char*>(workspace);
+    uint8_t* tflags = reinterpret_cast<uint8_t*>(wsb + z.flags_off);
+    uint32_t* tlist = reinterpret_cast<uint32_t*>(wsb + z.list_off);
+    uint32_t* tcount = reinterpret_cast<uint32_t*>(wsb + z.count_off);
+    hipLaunchKernelGGL(tile_flags_kernel, dim3(static_cast<unsigned>(ceil_div_ll(z.tiles, kTilesPerFlagWg))),
+                       dim3(kTileFlagThreads), 0, s, g_rgb, g_sigma, M, z.tiles, p.dense_bwd, tflags);
+    NR_LAUNCH_CHECK("nr_mlp_backward_dx (tile flags)");
+    hipLaunchKernelGGL(tile_list_kernel, dim3(1), dim3(kTileListThreads), 0, s, tflags, z.tiles, tlist, tcount);
+    NR_LAUNCH_CHECK("nr_mlp_backward_dx (tile list)");
     BwdArgs b;
     std::memset(&b, 0, sizeof(b));
     b.packed = static_cast<const char*>(packed);
@@ -3003,6 +2931,8 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     b.ws = static_cast<char*>(workspace);
     b.M = M;
     b.tiles = z.tiles;
+    b.list = tlist;
+    b.count = tcount;
     b.L = p.L;
     b.Ld = p.Ld;
     b.n_layers = p.n_layers;
@@ -3047,6 +2977,9 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
         r.ws = b.ws;
         r.M = M;
         r.tiles = z.tiles;
+        r.list = tlist;
+        r.count = tcount;
+        r.scratch_tile = z.tiles_alloc - 1;
         r.n_layers = n;
         r.base = p.lin[n + 1].pk_bwdr;
         r.vrgb = p.vrgb;
@@ -3069,6 +3002,17 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
         return input_grads16(p, z, b.packed, x, d, g_x, g_d, b.ws, M, s);
     }
     if (p.prec != NR_PREC_FP32 && !wx) return chain16();
+    if (!p.dense_bwd) {
+        // the chain writes g_x / g_d of the active tiles only: the rest are exactly zero
+        for (float* g : {g_x, g_d})
+            if (g) {
+                const hipError_t e = hipMemsetAsync(g, 0, sizeof(float) * 3 * static_cast<size_t>(M), s);
+                if (e != hipSuccess) {
+                    set_error("nr_mlp_backward_dx: %s", hipGetErrorString(e));
+                    return static_cast<int>(e);
+                }
+            }
+    }
     if (p.prec == NR_PREC_BF16) return launch_bwd<NR_PREC_BF16, true>(p, b, s);
     if (p.prec == NR_PREC_FP16) return launch_bwd<NR_PREC_FP16, true>(p, b, s);
     return wx ? launch_bwd<NR_PREC_FP32, true>(p, b, s) : launch_bwd<NR_PREC_FP32, false>(p, b, s);
@@ -3089,6 +3033,8 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
     std::memset(&w, 0, sizeof(w));
     w.slabs = reinterpret_cast<float*>(ws + z.slab_off);
     w.tiles = z.tiles;
+    w.list = reinterpret_cast<const uint32_t*>(ws + z.list_off);  // written by nr_mlp_backward_dx
+    w.count = reinterpret_cast<const uint32_t*>(ws + z.count_off);
     w.njobs = p.n_jobs;
     int nwg = 0;
     NR_REQUIRE(p.n_jobs <= 32 && z.max_chunks < 2048, "nr_mlp_backward_dw: %d jobs x %d chunks beyond the map",
@@ -3099,7 +3045,7 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
                 NR_REQUIRE(nwg < kDwMaxWgs, "nr_mlp_backward_dw: more than %d workgroups", kDwMaxWgs);
                 w.wg_map[nwg++] = static_cast<uint16_t>(j | c << 5);
             }
-    for (int j = 0; j < p.n_jobs; ++j) w.job_tpc[j] = static_cast<int>(ceil_div_ll(z.tiles, z.job_chunks[j]));
+    for (int j = 0; j < p.n_jobs; ++j) w.job_chunks[j] = z.job_chunks[j];
     w.slab_floats_per_chunk = p.slab_floats_per_chunk;
     int max_blk = 0;
     for (int j = 0; j < p.n_jobs; ++j) {
@@ -3193,103 +3139,10 @@ int nr_mlp_backward_reduce(const NrMlpConfig* cfg, int64_t M, const void* worksp
     return NR_OK;
 }
 
-int nr_mlp_backward_dxdw(const NrMlpConfig* cfg, const void* packed, const float* params, const float* x,
-                         const float* d, int64_t M, const float* rgb, const float* sigma, const void* saved,
-                         const float* g_rgb, const float* g_sigma, float* g_x, float* g_d, void* workspace,
-                         nr_stream_t stream) {
-    MlpPlan p;
-    if (!plan_or_error(cfg, &p)) return NR_EARG;
-    NR_REQUIRE(packed && params && x && rgb && sigma && saved && g_rgb && g_sigma && workspace && M >= 0,
-               "nr_mlp_backward_dxdw: null pointer");
-    NR_REQUIRE(!g_d || (d && p.use_vd), "nr_mlp_backward_dxdw: g_d needs d and use_view_dirs");
-    NR_REQUIRE((reinterpret_cast<uintptr_t>(workspace) & 15) == 0 && (reinterpret_cast<uintptr_t>(saved) & 15) == 0,
-               "nr_mlp_backward_dxdw: saved and workspace must be 16-byte aligned");
-    if (M == 0) return NR_OK;
-    NR_REQUIRE(M <= (int64_t{1} << 36), "nr_mlp_backward_dxdw: M beyond 2^36 samples");
-    const hipStream_t s = static_cast<hipStream_t>(stream);
-    const MlpSizes z = make_sizes(p, M);
-    PipeArgs a;  // ~3 KB of kernel arguments, copied by the launch
-    std::memset(&a, 0, sizeof(a));
-    int NX = 0;
-    const bool layout = pipe_layout(p, z, a, NX);
-    a.npipe = z.chunks;
-    const int cus = device_cus();
-    bool launched = false;
-    if (layout && cus > 0 && a.npipe * a.nstage <= cus && M <= kPipeMaxM) {
-        char* ws = static_cast<char*>(workspace);
-        a.packed = static_cast<const char*>(packed);
-        a.saved = static_cast<const char*>(saved);
-        a.ws = ws;
-        a.rgb = rgb;
-        a.sigma = sigma;
-        a.g_rgb = g_rgb;
-        a.g_sigma = g_sigma;
-        a.gscale = grad_scale(p.prec);
-        a.pose = (g_x || g_d) ? 1 : 0;
-        a.M = M;
-        a.tiles = z.tiles;
-        a.tpp = static_cast<int>(ceil_div_ll(z.tiles, z.chunks));  // = the split dW's tiles_per_chunk
-        a.slabs = reinterpret_cast<float*>(ws + z.slab_off);
-        a.slab_floats_per_chunk = p.slab_floats_per_chunk;
-        a.ring = ws + z.pipe_ring_off;
-        a.ring_pipe_bytes = z.pipe_ring_pipe_bytes;
-        a.status = reinterpret_cast<unsigned*>(ws + z.pipe_flags_off);
-        a.flags = a.status + kPipeStatusWordsHead;
-        a.mask_off = z.mask_off;
-        a.n_mask = p.n_mask;
-        a.sv_feat = z.saved_off[p.sv_feat];
-        a.sv_denc = z.saved_off[p.sv_denc];
-        a.sv_hc = z.saved_off[p.sv_hc];
-        a.sv_hlast = z.saved_off[SV_H0 + p.n_layers - 1];
-        a.vrgb = p.vrgb;
-        a.vhead = p.vhead;
-        // every flag / status word starts at 0 in every call (a memset node under capture)
-        const hipError_t e = hipMemsetAsync(ws + z.pipe_flags_off, 0, static_cast<size_t>(z.pipe_flags_bytes), s);
-        if (e != hipSuccess) {
-            set_error("nr_mlp_backward_dxdw: %s", hipGetErrorString(e));
-            return static_cast<int>(e);
-        }
-        const int rc = p.prec == NR_PREC_BF16 ? launch_pipe<NR_PREC_BF16>(p, a, NX, s, &launched)
-                                              : launch_pipe<NR_PREC_FP16>(p, a, NX, s, &launched);
-        if (rc) return rc;
-    }
-    if (!launched) {
-        // outside the pipeline's envelope (fp32, several skips, too few CUs): the split backward
-        const int rc = nr_mlp_backward_dx(cfg, packed, params, x, d, M, rgb, sigma, saved, g_rgb, g_sigma, g_x, g_d,
-                                          workspace, stream);
-        if (rc) return rc;
-        return nr_mlp_backward_dw(cfg, M, saved, workspace, stream);
-    }
-    if (g_x || g_d) return input_grads16(p, z, static_cast<const char*>(packed), x, d, g_x, g_d,
-                                         static_cast<const char*>(workspace), M, s);
-    return NR_OK;
-}
-
-int nr_mlp_backward_pipelined(const NrMlpConfig* cfg, int64_t M) {
-    MlpPlan p;
-    if (!plan_or_error(cfg, &p) || M <= 0) return 0;
-    const MlpSizes z = make_sizes(p, M);
-    PipeArgs a;
-    std::memset(&a, 0, sizeof(a));
-    int NX = 0;
-    if (!pipe_layout(p, z, a, NX)) return 0;
-    a.npipe = z.chunks;
-    const int cus = device_cus();
-    if (!(cus > 0 && a.npipe * a.nstage <= cus && M <= kPipeMaxM)) return 0;
-    // the same instance and residency checks nr_mlp_backward_dxdw makes before it launches
-    bool ok = false;
-    if (p.prec == NR_PREC_BF16)
-        launch_pipe<NR_PREC_BF16>(p, a, NX, nullptr, &ok, false);
-    else
-        launch_pipe<NR_PREC_FP16>(p, a, NX, nullptr, &ok, false);
-    return ok ? 1 : 0;
-}
-
-int64_t nr_mlp_pipe_status_offset(const NrMlpConfig* cfg, int64_t M) {
+int64_t nr_mlp_active_tiles_offset(const NrMlpConfig* cfg, int64_t M) {
     MlpPlan p;
     if (!plan_or_error(cfg, &p) || M <= 0) return -1;
-    const MlpSizes z = make_sizes(p, M);
-    return p.fpb == 2 ? z.pipe_flags_off : -1;
+    return make_sizes(p, M).count_off;
 }
 
 int nr_mlp_backward(const NrMlpConfig* cfg, const void* packed, const float* params, const float* x, const float* d,
@@ -3297,8 +3150,7 @@ int nr_mlp_backward(const NrMlpConfig* cfg, const void* packed, const float* par
                     const float* g_sigma, float* g_params, float* g_x, float* g_d, void* workspace,
                     nr_stream_t stream) {
     NR_REQUIRE(g_params, "nr_mlp_backward: null g_params");
-    // the split form (dX chain, dW GEMM), as noisy_src's default; nr_mlp_backward_dxdw is
-    // the layer-pipelined alternative for callers that choose it
+    // the split form: dX chain (dz images), then the dW GEMM over them
     int rc = nr_mlp_backward_dx(cfg, packed, params, x, d, M, rgb, sigma, saved, g_rgb, g_sigma, g_x, g_d, workspace,
                                 stream);
     if (rc) return rc;

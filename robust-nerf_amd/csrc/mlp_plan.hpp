@@ -100,6 +100,7 @@ struct ReduceRange {
 
 struct MlpPlan {
     int L, Ld, n_layers, use_vd, prec;
+    int dense_bwd;                    // NrMlpConfig.dense_backward: every tile through the backward
     uint32_t skips;
     int pos_dim, dir_dim, XB, DB;
     int64_t param_count;
@@ -141,29 +142,13 @@ struct MlpSizes {
     int64_t mask_off;                  // bytes
     int64_t saved_bytes;
     int64_t ws_off[kMaxTrunk + 3];     // bytes
-    int chunks;                        // dW split over sample tiles (= pipelines of the fused backward)
+    int chunks;                        // dW split over sample tiles
     int job_chunks[kMaxJobs];          // dW workgroups of each job (16-bit: all = chunks; fp32: by cost)
     int max_chunks;                    // per-chunk slab sets allocated (the largest job_chunks)
     int64_t slab_off;                  // bytes
-    // fused 16-bit backward (mlp_pipe.inc): status + flag words (zeroed every call), then
-    // the dz rings, [pipeline][edge][slot] 16-KB tiles; edges = dz_0 .. dz_{n-1}, dz_feat
-    int pipe_edges;
-    int64_t pipe_flags_off, pipe_flags_bytes;  // bytes
-    int64_t pipe_ring_off, pipe_ring_pipe_bytes;
+    int64_t flags_off, list_off, count_off;  // bytes: active-tile flags (u8), list (u32), count (u32)
     int64_t ws_bytes;
 };
-
-// ring slots per edge and 32-bit flag words per (pipeline, edge) of the fused backward
-#ifndef NR_PIPE_RING
-#define NR_PIPE_RING 32
-#endif
-constexpr int kPipeRingSlots = NR_PIPE_RING;
-constexpr int kPipeFlagWordsPerEdge = 128;
-#ifdef NR_PIPE_PROF
-constexpr int kPipeStatusWordsHead = 64 + 512 * 32;  // + per-workgroup timing records (diagnostic builds)
-#else
-constexpr int kPipeStatusWordsHead = 64;
-#endif
 
 MlpSizes make_sizes(const MlpPlan& p, int64_t M);
 

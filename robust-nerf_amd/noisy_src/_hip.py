@@ -40,6 +40,7 @@ class NrMlpConfig(ctypes.Structure):
         ("skip_mask", c_u32),
         ("use_view_dirs", c_i),
         ("precision", c_i),
+        ("dense_backward", c_i),
     ]
 
 
@@ -100,10 +101,7 @@ _SIGNATURES = {
                                  c_vp, c_vp]),
     "nr_mlp_backward_dw": (c_i, [_cfg_p, c_i64, c_vp, c_vp, c_vp]),
     "nr_mlp_backward_reduce": (c_i, [_cfg_p, c_i64, c_vp, c_vp, c_vp]),
-    "nr_mlp_backward_dxdw": (c_i, [_cfg_p, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                   c_vp, c_vp]),
-    "nr_mlp_backward_pipelined": (c_i, [_cfg_p, c_i64]),
-    "nr_mlp_pipe_status_offset": (c_i64, [_cfg_p, c_i64]),
+    "nr_mlp_active_tiles_offset": (c_i64, [_cfg_p, c_i64]),
     "nr_sumsq_workspace_bytes": (c_i64, []),
     "nr_sumsq": (c_i, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "nr_adam_step": (c_i, [c_vp, c_vp, c_vp, c_vp, c_i64, c_d, c_d, c_d, c_d, c_i64, c_vp, c_f, c_vp]),

@@ -231,7 +231,8 @@ class Trainer:
              t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         self.optimizer.zero_grad(set_to_none=True)
         cs = None
-        if self.coarse_stream is not False and self.model_fine is not None and rays_o.is_cuda:
+        if (self.coarse_stream is not False and self.model_fine is not None and rays_o.is_cuda
+                and self.render_config.use_hierarchical):
             # created on the first eager step (a GraphedTrainer warms up eagerly), not
             # inside a capture
             if self._cstream is None or self._cstream.device != rays_o.device:
@@ -245,7 +246,10 @@ class Trainer:
 
         def coarse_backward(out_c):
             # on the coarse stream: the coarse loss and its backward, beside the fine
-            # forward (loss = loss_c + loss_f sends exactly d loss_c to the coarse net)
+            # forward (loss = loss_c + loss_f sends exactly d loss_c to the coarse net);
+            # target_rgb may come from the current stream's pool (record_stream: see
+            # render_rays)
+            target_rgb.record_stream(torch.cuda.current_stream(target_rgb.device))
             early["loss_c"] = ops.mse_loss(out_c["rgb_map"], target_rgb, gs)
             early["loss_c"].backward(ops.unit_grad(rays_o.device))
 

@@ -54,9 +54,10 @@ class PositionalEncoding(nn.Module):
         return ops.positional_encoding(x, self.num_freqs, self.include_input, self.log_sampling)
 
 
-# NR_MLP_BACKWARD=split selects the split dX + dW backward instead of the fused
-# layer-pipelined launch (A/B comparisons; both give bit-identical gradients)
-_SPLIT_BACKWARD = os.environ.get("NR_MLP_BACKWARD", "split") == "split"
+# NR_MLP_DENSE_BACKWARD=1 runs every 32-sample tile through the backward (the dense
+# reference form, for A/B runs); by default tiles whose incoming gradient is exactly
+# zero are skipped (csrc/mlp.hip, tile_flags_kernel: identical gradients)
+_DENSE_BACKWARD = os.environ.get("NR_MLP_DENSE_BACKWARD", "0") not in ("", "0")
 
 
 def _precision_code(p: str) -> int:
@@ -112,15 +113,14 @@ class _MLPFunction(torch.autograd.Function):
             st, tag = _hip.stream_ptr(), f"[M={M}]"
             args = (cfg, ptr(packed), ptr(flat), ptr(xc), ptr(dc) if ctx.has_d else None, M, ptr(rgb), ptr(sigma),
                     ptr(saved), ptr(g_rgb), ptr(g_sigma), ptr(g_x), ptr(g_d), ptr(ws), st)
-            if _SPLIT_BACKWARD:
-                # the split form: dX chain (dz images in HBM), then the dW GEMM over them
-                call("nr_mlp_backward_dx", *args, tag=tag)
-                call("nr_mlp_backward_dw", cfg, M, ptr(saved), ptr(ws), st, tag=tag)
-            else:
-                # one layer-pipelined launch (16-bit; the library runs the split form where
-                # the pipeline does not apply, e.g. fp32): bit-identical slabs
-                call("nr_mlp_backward_dxdw", *args, tag=tag)
+            # dX chain over the active tiles (dz images in HBM), then the dW GEMM over them
+            call("nr_mlp_backward_dx", *args, tag=tag)
+            call("nr_mlp_backward_dw", cfg, M, ptr(saved), ptr(ws), st, tag=tag)
             call("nr_mlp_backward_reduce", cfg, M, ptr(ws), ptr(gflat), st, tag=tag)
+            if net._tile_counts is not None:
+                # diagnostics (bench.py): the active-tile count this backward ran on
+                off = int(_hip.load().nr_mlp_active_tiles_offset(cfg, M))
+                net._tile_counts.append((M, ws[off:off + 4].view(torch.int32).clone()))
         else:
             gflat.zero_()
         net._last_gflat = gflat  # FusedAdam's fast path reads the flat gradient directly
@@ -199,7 +199,8 @@ class NeRF(nn.Module):
         self._nr_cfg = NrMlpConfig(
             pos_freqs=config.pos_freqs, dir_freqs=config.dir_freqs, hidden=config.hidden_dim,
             n_layers=config.num_hidden_layers, skip_mask=skip_mask, use_view_dirs=int(bool(config.use_view_dirs)),
-            precision=_precision_code(getattr(config, "precision", "fp32")))
+            precision=_precision_code(getattr(config, "precision", "fp32")),
+            dense_backward=int(_DENSE_BACKWARD))
         self._param_count = sum(p.numel() for p in self.parameters())
         _check_supported(self._nr_cfg, config, self._param_count)
         self._flat: Optional[torch.Tensor] = None
@@ -209,6 +210,8 @@ class NeRF(nn.Module):
         self._last_gflat: Optional[torch.Tensor] = None  # the last backward's flat gradient
         # called with the flat gradient as soon as the backward has produced it
         self._grad_ready_hook = None
+        # a list: every backward appends (M, its device count of active 32-sample tiles)
+        self._tile_counts: Optional[list] = None
 
     # -- flat parameter buffer -------------------------------------------------
     @property

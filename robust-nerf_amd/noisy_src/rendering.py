@@ -70,6 +70,12 @@ def render_rays(model_coarse: NeRF, model_fine: Optional[NeRF], rays_o: torch.Te
     if coarse_stream is not None:
         main = torch.cuda.current_stream(rays_o.device)
         coarse_stream.wait_stream(main)
+        # these blocks come from the current stream's pool and the coarse chain (its
+        # backward included, which may still run after this function returns) reads
+        # them on the coarse stream: without the record the allocator could hand them
+        # to the fine chain's allocations while the coarse kernels still read them
+        for t in (pts, vd, z_c, rays_d):
+            t.record_stream(coarse_stream)
         with torch.cuda.stream(coarse_stream):
             rgb_c, sigma_c = model_coarse(pts.reshape(-1, 3), vd)
             out_c = raw2outputs(rgb_c.reshape(N_rays, Nc, 3), sigma_c.reshape(N_rays, Nc, 1), z_c, rays_d,

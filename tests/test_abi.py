@@ -56,3 +56,20 @@ def test_plan_sizes_match_reference_model():
                            precision=0)
     assert L.nr_mlp_param_count(ctypes.byref(bad)) == -1
     assert "hidden_dim" in _hip.last_error()
+
+
+def test_struct_layouts_match_header():
+    """The ctypes mirrors list the header's struct fields in order (NrMlpConfig gained
+    dense_backward in ABI 5)."""
+    text = HEADER.read_text()
+    for name, mirror in (("NrMlpConfig", _hip.NrMlpConfig), ("NrAdamSpan", _hip.NrAdamSpan)):
+        body = re.search(r"typedef struct " + name + r" \{(.*?)\} " + name + ";", text, re.S).group(1)
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        assert re.findall(r"(\w+)\s*;", body) == [f[0] for f in mirror._fields_], name
+
+
+def test_abi_version():
+    lib = _hip.lib_path()
+    if not lib.exists():
+        pytest.skip("library not built")
+    assert _hip.load().nr_abi_version() == 5

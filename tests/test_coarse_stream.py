@@ -56,6 +56,48 @@ def test_coarse_stream_eager_equals_one_stream(precision):
     _same(one, two)
 
 
+def test_coarse_stream_lagging_backward_equals_one_stream(monkeypatch):
+    """the coarse backward reads blocks of the main stream's pool (pts, view
+    dirs, z, rays_d, the targets) on the coarse stream, possibly after render_rays has
+    returned and dropped them.  A spin kernel ahead of the coarse loss makes that chain
+    lag far behind the fine one, whose allocations would take those blocks over without
+    the cross-stream record.  Large Nc, small Nf; still bit-identical."""
+    from noisy_src import engine
+    orig = engine.render_rays
+
+    def lagging(*args, coarse_backward=None, **kw):
+        if coarse_backward is not None:
+            cb = coarse_backward
+
+            def coarse_backward(out_c):
+                torch.cuda._sleep(20_000_000)  # ~10 ms of spinning on the coarse stream
+                cb(out_c)
+        return orig(*args, coarse_backward=coarse_backward, **kw)
+
+    monkeypatch.setattr(engine, "render_rays", lagging)
+    rc, (one, two) = _pair("bf16", 128, 16)
+    for k, b in enumerate(_batches(rc, 1024, 4, seed=5)):
+        l1 = float(one.step(*b)["loss"])
+        l2 = float(two.step(*b)["loss"])
+        assert l1 == l2, (k, l1, l2)
+    _same(one, two)
+
+
+def test_coarse_stream_needs_hierarchical():
+    """model_fine set but use_hierarchical=False renders no fine output; the
+    trainer then stays on one stream instead of failing on 'rgb_fine'."""
+    from noisy_src.config import ModelConfig, RenderConfig
+    from noisy_src.engine import Trainer
+    from noisy_src.model import create_nerf
+    rc = RenderConfig(num_samples=32, num_samples_fine=16, use_hierarchical=False)
+    torch.manual_seed(3)
+    mc, mf = create_nerf(ModelConfig(precision="bf16"))
+    tr = Trainer(mc.to(DEV), mf.to(DEV), rc, coarse_stream=True)
+    b = _batches(RenderConfig(num_samples=32, num_samples_fine=16), 256, 1)[0]
+    out = tr.step(*b)
+    assert not tr.last_step_coarse_stream and torch.isfinite(out["loss"])
+
+
 def test_coarse_stream_graph_equals_eager():
     """cfg #4's per-rank size (512 rays, 64c+128f): the two-branch graph replay equals the
     one-stream eager step bit for bit."""

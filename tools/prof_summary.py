@@ -30,17 +30,21 @@ ROOT = Path(__file__).resolve().parents[1]
 FAMILIES = {"mlp_fwd_kernel": "nr_mlp_forward", "mlp_bwd_kernel": "nr_mlp_backward_dx",
             "mlp_fwd_rbm_kernel": "nr_mlp_forward", "mlp_bwd_rbm_kernel": "nr_mlp_backward_dx",
             "mlp_dinput_kernel": "nr_mlp_backward_dx (input grads)",
-            "mlp_dw_kernel": "nr_mlp_backward_dw", "mlp_dw_reduce_kernel": "nr_mlp_backward_reduce",
-            "mlp_bwd_pipe_kernel": "nr_mlp_backward_dxdw"}
+            "mlp_dw_kernel": "nr_mlp_backward_dw", "mlp_dw_reduce_kernel": "nr_mlp_backward_reduce"}
 
 
 def source_hash() -> str:
     """sha1 over the HIP sources and the ABI header (bench.py computes the same hash, so
     it uses a kernel summary only when it was profiled from the benchmarked sources);
-    NR_SOURCE_HASH overrides it when re-summarising a trace taken from an older tree."""
+    NR_SOURCE_HASH overrides it when re-summarising a trace taken from an older tree, and
+    every row it writes then says so (``hash_overridden``, which bench.py refuses)."""
     import os
     if os.environ.get("NR_SOURCE_HASH"):
         return os.environ["NR_SOURCE_HASH"]
+    return computed_hash()
+
+
+def computed_hash() -> str:
     h = hashlib.sha1()
     files = sorted((ROOT / "robust-nerf_amd" / "csrc").glob("*")) + [ROOT / "include" / "nerf_hip.h"]
     for f in files:
@@ -69,10 +73,7 @@ def is_training_forward(name: str) -> bool:
 class MTracker:
     """M of every fused-MLP launch in stream order.  The forward / dX kernels run one
     32-sample tile per wave, so their grid gives M.  dW, its reduction and the input
-    gradients follow the backward launch of the same M.  The fused layer-pipelined
-    backward's grid is pipelines x stages (independent of M): it belongs to the training
-    forward of the same net, and autograd runs the backwards in reverse forward order
-    (fine before coarse), so each one pops the newest unmatched training forward."""
+    gradients follow the backward launch of the same M."""
 
     def __init__(self):
         self.last = 0
@@ -87,8 +88,6 @@ class MTracker:
                 self.fwd_stack.append(M)
             elif fam in ("mlp_bwd_kernel", "mlp_bwd_rbm_kernel") and self.fwd_stack:
                 self.fwd_stack.pop()
-        elif fam == "mlp_bwd_pipe_kernel":
-            M = self.fwd_stack.pop() if self.fwd_stack else self.last
         elif fam in ("mlp_dw_kernel", "mlp_dw_reduce_kernel", "mlp_dinput_kernel"):
             M = self.last
         self.last = M or self.last
@@ -111,13 +110,14 @@ def main(out_dir: str, tag: str, timed_steps: int = 0) -> None:
     with open(summ, "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["kernel", "precision", "grid_threads", "M_samples", "calls", "avg_ms", "median_ms", "total_ms",
-                    "timed_avg_ms", "source_hash"])
+                    "timed_avg_ms", "source_hash", "hash_overridden"])
         sh = source_hash()
+        over = "" if sh == computed_hash() else f"computed {computed_hash()}"
         for (k, g, M), v in sorted(rows.items(), key=lambda kv: -sum(kv[1])):
             timed = v[-timed_steps:] if (timed_steps and M and len(v) >= timed_steps) else []
             w.writerow([short(k), precision_of(k), g, M or "", len(v), f"{statistics.mean(v):.4f}",
                         f"{statistics.median(v):.4f}", f"{sum(v):.3f}",
-                        f"{statistics.mean(timed):.4f}" if timed else "", sh])
+                        f"{statistics.mean(timed):.4f}" if timed else "", sh, over])
     print(f"wrote {summ}")
 
     counters = defaultdict(lambda: defaultdict(list))
@@ -147,6 +147,7 @@ def main(out_dir: str, tag: str, timed_steps: int = 0) -> None:
         print("no PMC passes under", base, "- profiles/traffic.json left as it is")
         return
     out = {"source_hash": source_hash(),
+           **({"hash_overridden": f"computed {computed_hash()}"} if source_hash() != computed_hash() else {}),
            "source": f"profiles/{tag}: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
                      "python bench.py --steps 2 --warmup 1 --no-cpu-baseline; traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (median)",
            "kernels": recs,
