@@ -162,7 +162,7 @@ def test_trained_state_backward_matches_dense():
         for net in nets:
             net._tile_counts = None
             net._nr_cfg.dense_backward = 0
-        return float(loss), [torch.cat([p.grad.reshape(-1) for p in net.parameters()]).clone() for net in nets], counts
+        return float(loss.detach()), [torch.cat([p.grad.reshape(-1) for p in net.parameters()]).clone() for net in nets], counts
 
     # the incoming gradients themselves, for the expected counts
     from noisy_src import model as model_mod
