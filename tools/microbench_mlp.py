@@ -16,6 +16,12 @@ def bench(prec, M, reps=int(__import__("os").environ.get("MB_REPS", "20"))):
     saved = torch.empty(L.nr_mlp_saved_bytes(cfg, M), dtype=torch.uint8, device="cuda")
     ws = torch.empty(L.nr_mlp_workspace_bytes(cfg, M), dtype=torch.uint8, device="cuda")
     grgb = torch.randn(M, 3, device="cuda"); gs = torch.randn(M, 1, device="cuda")
+    # MB_ACTIVE=f: zero the incoming gradient of all but a fraction f of the 32-sample tiles
+    # (the trained-state regime: the backward then runs on the active tiles only)
+    f = float(__import__("os").environ.get("MB_ACTIVE", "1"))
+    if f < 1:
+        keep = (torch.rand((M + 31) // 32, device="cuda") < f).repeat_interleave(32)[:M]
+        grgb *= keep[:, None]; gs *= keep[:, None]
     gflat = torch.empty_like(flat)
     P = _hip.ptr
     fns = {
@@ -23,11 +29,10 @@ def bench(prec, M, reps=int(__import__("os").environ.get("MB_REPS", "20"))):
         "fwd_train": lambda: _hip.call("nr_mlp_forward", cfg, P(packed), P(flat), P(x), P(d), M, P(rgb), P(sig), P(saved), st),
         "bwd_dx": lambda: _hip.call("nr_mlp_backward_dx", cfg, P(packed), P(flat), P(x), P(d), M, P(rgb), P(sig), P(saved), P(grgb), P(gs), None, None, P(ws), st),
         "bwd_dw": lambda: _hip.call("nr_mlp_backward_dw", cfg, M, P(saved), P(ws), st),
-        "bwd_dxdw": lambda: _hip.call("nr_mlp_backward_dxdw", cfg, P(packed), P(flat), P(x), P(d), M, P(rgb), P(sig), P(saved), P(grgb), P(gs), None, None, P(ws), st),
         "bwd_reduce": lambda: _hip.call("nr_mlp_backward_reduce", cfg, M, P(ws), P(gflat), st),
     }
     out = {}
-    names = __import__("os").environ.get("MB_KERNELS", "fwd_infer,fwd_train,bwd_dx,bwd_dw,bwd_dxdw,bwd_reduce")
+    names = __import__("os").environ.get("MB_KERNELS", "fwd_infer,fwd_train,bwd_dx,bwd_dw,bwd_reduce")
     for name in names.split(","):
         fn = fns[name]
         fn(); torch.cuda.synchronize()
