@@ -125,11 +125,13 @@ int nr_gather_rays(const int64_t* idx, int64_t n_rays, int B,
                    nr_stream_t stream);
 
 /* ---- A5: sample_along_rays  (noisy_src/rays.py:145-210) ------------------
- * z (B,N); pts (B,N,3) nullable.  t_rand (B,N) nullable -> no perturbation. */
+ * z (B,N); pts (B,N,3) nullable.  t_rand (B,N) nullable -> no perturbation.
+ * viewdirs (B*N,3) nullable: rays_d / |rays_d| per sample (rendering.py:165), as
+ * nr_expand_viewdirs writes it.                                               */
 int nr_stratified_sample(const float* rays_o, const float* rays_d,
                          const float* t_rand, float near_, float far_,
                          int lindisp, int B, int N, float* z_vals, float* pts,
-                         nr_stream_t stream);
+                         float* viewdirs, nr_stream_t stream);
 
 /* ---- A6: PositionalEncoding.forward  (noisy_src/model.py:58-80) ----------
  * x (M,C) -> out (M, C*(include_input + 2L)) laid out [x | sin f0x | cos f0x | ...]. */
@@ -149,11 +151,13 @@ int nr_sample_pdf(const float* bins, const float* weights, const float* u,
 
 /* ---- A10: sample_hierarchical  (noisy_src/rays.py:282-333) ---------------
  * z_coarse (B,Nc), w_coarse (B,Nc) -> z_fine (B,Nc+Nf) = sort(cat(z, sample_pdf(
- * mid(z), w[:,1:-1], Nf, det))), pts_fine (B,Nc+Nf,3) nullable.  u nullable=det. */
+ * mid(z), w[:,1:-1], Nf, det))), pts_fine (B,Nc+Nf,3) nullable.  u nullable=det.
+ * viewdirs (B*(Nc+Nf),3) nullable, as in nr_stratified_sample.               */
 int nr_sample_hierarchical(const float* rays_o, const float* rays_d,
                            const float* z_coarse, const float* w_coarse,
                            const float* u, int B, int Nc, int Nf,
-                           float* z_fine, float* pts_fine, nr_stream_t stream);
+                           float* z_fine, float* pts_fine, float* viewdirs,
+                           nr_stream_t stream);
 
 /* ---- A8: raw2outputs  (noisy_src/rendering.py:20-116) --------------------
  * rgb (B,S,3), sigma (B,S), z (B,S), rays_d (B,3), sigma_noise (B,S) nullable
@@ -322,6 +326,23 @@ int nr_viewdirs_bwd(const float* rays_d, const float* g_viewdirs, int B,
  * loss_out (device scalar, OVERWRITTEN) may be NULL. */
 int nr_mse_fwd_bwd(const float* pred, const float* target, int B, float scale,
                    float* loss_out, float* g_pred, nr_stream_t stream);
+/* The training form of raw2outputs + the MSE loss (rendering.py:20-116 then
+ * train.py:89/98): the composite forward (outputs as nr_composite_fwd), the loss
+ * (device scalar, OVERWRITTEN) against target (B,3), and the backward of
+ * grad_scale * loss (g_rgb, g_sigma OVERWRITTEN; g_rays_d nullable, ACCUMULATED) in one
+ * wave per ray -- gradients bit-identical to nr_composite_fwd, nr_mse_fwd_bwd and
+ * nr_composite_bwd in sequence.  ticket (nullable): a device uint32 that is 0 before
+ * the call and is left 0; with it (and B <= 1024) the launch's last workgroup sums the
+ * loss, otherwise a second launch does.  Calls sharing a ticket must not run concurrently.
+ * workspace: nr_composite_mse_workspace_bytes(B).                                 */
+int64_t nr_composite_mse_workspace_bytes(int B);
+int nr_composite_mse(const float* rgb, const float* sigma, const float* z,
+                     const float* rays_d, const float* sigma_noise,
+                     const float* target, int B, int S, int white,
+                     float grad_scale, float* rgb_map, float* depth_map,
+                     float* acc_map, float* weights, float* loss, float* g_rgb,
+                     float* g_sigma, float* g_rays_d, uint32_t* ticket,
+                     void* workspace, nr_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -49,6 +49,8 @@ constexpr int kWave = 64;
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ inline long long ceil_div_ll(long long a, long long b) { return (a + b - 1) / b; }
 
+__device__ __forceinline__ float norm3(float x, float y, float z) { return sqrtf(x * x + y * y + z * z); }
+
 // Grid for a grid-stride memory-bound kernel (cdna_hip_programming.md G11).
 inline int stream_grid(long long work, int block) {
     long long g = ceil_div_ll(work, block);

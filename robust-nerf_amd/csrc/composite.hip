@@ -304,6 +304,221 @@ __global__ __launch_bounds__(256) void composite_bwd_wave_kernel(
     }
 }
 
+// One ray of composite_mse_wave_kernel (lane = the wave's lane).
+__device__ __forceinline__ void composite_mse_ray(const float* rgb, const float* sigma, const float* z, const float* rd,
+                                                  const float* noise, const float* target, int b, int S, int K,
+                                                  int white, float inv, float scale, float* rgb_map, float* depth,
+                                                  float* acc, float* weights, float* sqerr, float* g_rgb,
+                                                  float* g_sigma, float* g_rd, int lane) {
+    const float dx = rd[3 * b], dy = rd[3 * b + 1], dz = rd[3 * b + 2];
+    const float dnorm = sqrtf(dx * dx + dy * dy + dz * dz);
+    const int64_t base = static_cast<int64_t>(b) * S;
+    const int i0 = lane * K;
+    float al[kCompK], tt[kCompK], ee[kCompK], sg[kCompK], dr[kCompK], L[kCompK], c[kCompK][3], zz[kCompK];
+    float P = 1.0f;
+#pragma unroll
+    for (int k = 0; k < kCompK; ++k) {
+        al[k] = 0.f;
+        tt[k] = 1.0f;
+        ee[k] = 1.0f;
+        sg[k] = 0.f;
+        dr[k] = 0.f;
+        zz[k] = 0.f;
+        c[k][0] = c[k][1] = c[k][2] = 0.f;
+        L[k] = P;
+        const int i = i0 + k;
+        if (k < K && i < S) {
+            const SampleTerms st = sample_terms(sigma, z, noise, base, i, S, dnorm);
+            al[k] = st.alpha;
+            tt[k] = 1.0f - st.alpha + 1e-10f;
+            ee[k] = st.e;
+            sg[k] = st.sig;
+            dr[k] = st.delta_raw;
+            zz[k] = z[base + i];
+            const int64_t q = 3 * (base + i);
+            c[k][0] = rgb[q];
+            c[k][1] = rgb[q + 1];
+            c[k][2] = rgb[q + 2];
+            P = P * tt[k];
+        }
+    }
+    float incl = P;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const float o = __shfl_up(incl, d);
+        if (lane >= d) incl *= o;
+    }
+    float E = __shfl_up(incl, 1);
+    if (lane == 0) E = 1.0f;
+    // forward
+    float r = 0.f, g = 0.f, bl = 0.f, dd = 0.f, a = 0.f;
+#pragma unroll
+    for (int k = 0; k < kCompK; ++k) {
+        const int i = i0 + k;
+        if (k < K && i < S) {
+            const float w = al[k] * (E * L[k]);
+            if (weights) weights[base + i] = w;
+            r += w * c[k][0];
+            g += w * c[k][1];
+            bl += w * c[k][2];
+            dd += w * zz[k];
+            a += w;
+        }
+    }
+    r = wave_sum(r);
+    g = wave_sum(g);
+    bl = wave_sum(bl);
+    dd = wave_sum(dd);
+    a = wave_sum(a);
+    if (white) {
+        r = r + (1.0f - a);
+        g = g + (1.0f - a);
+        bl = bl + (1.0f - a);
+    }
+    // loss seed
+    const float d0 = r - target[3 * b], d1 = g - target[3 * b + 1], d2 = bl - target[3 * b + 2];
+    const float gr = (2.0f * d0) * inv * scale, gg = (2.0f * d1) * inv * scale, gb = (2.0f * d2) * inv * scale;
+    if (lane == 0) {
+        rgb_map[3 * b] = r;
+        rgb_map[3 * b + 1] = g;
+        rgb_map[3 * b + 2] = bl;
+        if (depth) depth[b] = dd;
+        if (acc) acc[b] = a;
+        sqerr[b] = (d0 * d0 + d1 * d1) + d2 * d2;
+    }
+    // backward (composite_bwd_wave_kernel with g_depth = g_acc = g_w = 0)
+    const float gd = 0.f;
+    const float ga = 0.f - (white ? (gr + gg) + gb : 0.f);
+    float GG[kCompK];
+#pragma unroll
+    for (int k = 0; k < kCompK; ++k) {
+        GG[k] = 0.f;
+        if (k < K && i0 + k < S) GG[k] = ((gr * c[k][0] + gg * c[k][1]) + gb * c[k][2]) + gd * zz[k] + ga;
+    }
+    float A[kCompK], Bc[kCompK];
+    float an = 0.f, bn = 1.0f;
+#pragma unroll
+    for (int k = kCompK - 1; k >= 0; --k) {
+        if (k < K) {
+            if (k == K - 1) {
+                an = 0.f;
+                bn = 1.0f;
+            } else {
+                an = GG[k + 1] * al[k + 1] + tt[k + 1] * an;
+                bn = tt[k + 1] * bn;
+            }
+        }
+        A[k] = an;
+        Bc[k] = bn;
+    }
+    float qa = GG[0] * al[0] + tt[0] * A[0];
+    float qb = tt[0] * Bc[0];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const float oa = __shfl_down(qa, d), ob = __shfl_down(qb, d);
+        if (lane + d < 64) {
+            qa = qa + qb * oa;
+            qb = qb * ob;
+        }
+    }
+    float X = __shfl_down(qa, 1);
+    if (lane == 63) X = 0.f;
+    float g_norm = 0.f;
+#pragma unroll
+    for (int k = 0; k < kCompK; ++k) {
+        const int i = i0 + k;
+        if (k < K && i < S) {
+            const float Ti = E * L[k];
+            const float w = al[k] * Ti;
+            const int64_t q = 3 * (base + i);
+            g_rgb[q] = gr * w;
+            g_rgb[q + 1] = gg * w;
+            g_rgb[q + 2] = gb * w;
+            const float R = A[k] + Bc[k] * X;
+            const float g_alpha = Ti * (GG[k] - R);
+            const float g_x = -g_alpha * ee[k];
+            g_sigma[base + i] = (sg[k] > 0.f) ? -g_x * (dr[k] * dnorm) : 0.f;
+            g_norm += g_x * (-sg[k] * dr[k]);
+        }
+    }
+    g_norm = wave_sum(g_norm);
+    if (g_rd && lane == 0) {
+        g_rd[3 * b] += g_norm * dx / dnorm;
+        g_rd[3 * b + 1] += g_norm * dy / dnorm;
+        g_rd[3 * b + 2] += g_norm * dz / dnorm;
+    }
+}
+
+
+// The last workgroup to finish (an agent-scope ticket; the recipe of
+// cdna_hip_programming.md §6 Guideline 16: plain stores, release fence, relaxed
+// fetch_add, acquire fence in the reducer) sums the per-ray squared errors in a fixed
+// order and leaves the ticket at 0 for the next call.
+__device__ __forceinline__ void sum_loss_last_block(const float* sqerr, int B, float inv, unsigned* ticket,
+                                                    float* loss) {
+    __shared__ float part[5];  // [0..3]: wave sums, [4]: the "last" flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        part[4] = t == gridDim.x - 1 ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (part[4] == 0.f) return;  // workgroup-uniform
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    float sum = 0.f;
+    for (int i = threadIdx.x; i < B; i += blockDim.x) sum += sqerr[i];
+    sum = wave_sum(sum);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float tot = 0.f;
+        for (int w = 0; w < static_cast<int>(blockDim.x >> 6); ++w) tot += part[w];
+        *loss = tot * inv;
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Training form: raw2outputs (rendering.py:20-116) + the MSE loss seed (train.py:89,98:
+// mean over 3B of (rgb_map - target)^2, gradient 2 (rgb_map - target) / 3B * scale) + the
+// backward of both, in one wave-per-ray pass.  Every value is the expression
+// composite_fwd_wave_kernel, mse_kernel and composite_bwd_wave_kernel evaluate (the
+// backward's depth / acc / weight terms are the zeros those kernels read for absent
+// gradients), so g_rgb / g_sigma / g_rd are bit-identical to the three launches.  The
+// loss is summed per ray (sqerr), then over the rays by the last workgroup (ticket) or,
+// without a ticket, by loss_sum_kernel.
+__global__ __launch_bounds__(256) void composite_mse_wave_kernel(
+    const float* rgb, const float* sigma, const float* z, const float* rd, const float* noise, const float* target,
+    int B, int S, int K, int white, float inv, float scale, float* rgb_map, float* depth, float* acc, float* weights,
+    float* sqerr, float* g_rgb, float* g_sigma, float* g_rd, unsigned* ticket, float* loss) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (b < B) composite_mse_ray(rgb, sigma, z, rd, noise, target, b, S, K, white, inv, scale, rgb_map, depth, acc,
+                                 weights, sqerr, g_rgb, g_sigma, g_rd, lane);
+    if (ticket) sum_loss_last_block(sqerr, B, inv, ticket, loss);
+}
+
+// loss = inv * sum of the per-ray squared errors, in a fixed order.  One block.
+__global__ __launch_bounds__(1024) void loss_sum_kernel(const float* sqerr, int B, float inv, float* loss) {
+    __shared__ float part[16];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < B; i += blockDim.x) s += sqerr[i];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float tot = 0.f;
+        for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) tot += part[i];
+        *loss = tot * inv;
+    }
+}
+
 // loss = mean((p - t)^2) over n = 3B; g = 2 (p - t) / n * scale.  One block.
 __global__ void mse_kernel(const float* p, const float* t, int n, float scale, float* loss, float* g) {
     __shared__ float part[16];
@@ -363,6 +578,42 @@ int nr_composite_bwd(const float* rgb, const float* sigma, const float* z, const
     NR_LAUNCH_CHECK("nr_composite_bwd");
     return NR_OK;
 }
+
+int nr_composite_mse(const float* rgb, const float* sigma, const float* z, const float* rd, const float* noise,
+                     const float* target, int B, int S, int white, float scale, float* rgb_map, float* depth,
+                     float* acc, float* weights, float* loss, float* g_rgb, float* g_sigma, float* g_rd,
+                     unsigned* ticket, void* workspace, nr_stream_t stream) {
+    NR_REQUIRE(rgb && sigma && z && rd && target && rgb_map && loss && g_rgb && g_sigma && workspace && B > 0 && S > 0,
+               "nr_composite_mse: bad arguments");
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    float* sqerr = static_cast<float*>(workspace);
+    const float inv = 1.0f / static_cast<float>(3 * B);
+    // the in-launch loss sum pays up to ~256 workgroups; beyond, the agent-scope release and
+    // ticket of every workgroup cost more than a second one-block launch (measured: 1024
+    // workgroups, 4096 rays, 61 vs 26 + 5 us)
+    if (ticket && ceil_div(B, 4) > 256) ticket = nullptr;
+    if (S <= 64 * kCompK) {
+        hipLaunchKernelGGL(composite_mse_wave_kernel, dim3(ceil_div(B, 4)), dim3(256), 0, s, rgb, sigma, z, rd, noise,
+                           target, B, S, (S + 63) / 64, white, inv, scale, rgb_map, depth, acc, weights, sqerr, g_rgb,
+                           g_sigma, g_rd, ticket, loss);
+        NR_LAUNCH_CHECK("nr_composite_mse");
+        if (!ticket) {
+            hipLaunchKernelGGL(loss_sum_kernel, dim3(1), dim3(1024), 0, s, sqerr, B, inv, loss);
+            NR_LAUNCH_CHECK("nr_composite_mse (loss)");
+        }
+        return NR_OK;
+    }
+    // long rays: the three separate passes (the seed gradient lives in the workspace)
+    float* g_map = sqerr + B;
+    int rc = nr_composite_fwd(rgb, sigma, z, rd, noise, B, S, white, rgb_map, depth, acc, weights, stream);
+    if (rc) return rc;
+    rc = nr_mse_fwd_bwd(rgb_map, target, B, scale, loss, g_map, stream);
+    if (rc) return rc;
+    return nr_composite_bwd(rgb, sigma, z, rd, noise, B, S, white, g_map, nullptr, nullptr, nullptr, g_rgb, g_sigma,
+                            g_rd, stream);
+}
+
+int64_t nr_composite_mse_workspace_bytes(int B) { return B > 0 ? int64_t{16} * B : 0; }
 
 int nr_mse_fwd_bwd(const float* pred, const float* target, int B, float scale, float* loss, float* g,
                    nr_stream_t stream) {

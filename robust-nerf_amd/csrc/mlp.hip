@@ -1189,6 +1189,50 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     }
 }
 
+// The dW kernel's work list, built by the FIRST workgroup of the dX launch after its own
+// tiles (off the critical path: the other workgroups keep the GPU busy): the segment
+// lists of tile_flags_kernel concatenated in segment order -- every active tile once, in
+// increasing order -- and their total.  sh: LDS scratch of 2 * blockDim.x + 16 words.
+__device__ void build_tile_list(const uint32_t* __restrict__ seg_list, const uint32_t* __restrict__ seg_count,
+                                int64_t nseg, uint32_t* __restrict__ list, uint32_t* __restrict__ count,
+                                uint32_t* sh) {
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
+    uint32_t* wsum = sh;           // [16]
+    uint32_t* starts = sh + 16;    // [nt]
+    uint32_t* cnts = starts + nt;  // [nt]
+    __syncthreads();
+    uint32_t base = 0;
+    for (int64_t s0 = 0; s0 < nseg; s0 += nt) {
+        const int64_t sg = s0 + tid;
+        const uint32_t c = sg < nseg ? seg_count[sg] : 0u;
+        uint32_t incl = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d);
+            if (lane >= d) incl += o;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        for (int q = 0; q < nw; ++q) {
+            const uint32_t v = wsum[q];
+            before += q < wv ? v : 0u;
+            total += v;
+        }
+        starts[tid] = base + before + incl - c;
+        cnts[tid] = c;
+        __syncthreads();
+        // one wave per segment: lane l copies entry l (coalesced)
+        const int nj = static_cast<int>(nseg - s0 < nt ? nseg - s0 : nt);
+        for (int j = wv; j < nj; j += nw) {
+            if (static_cast<uint32_t>(lane) < cnts[j]) list[starts[j] + lane] = seg_list[(s0 + j) * kSegTiles + lane];
+        }
+        base += total;
+        __syncthreads();
+    }
+    if (tid == 0) *count = base;
+}
+
 #include "mlp_fwd_rbm.inc"
 #include "mlp_bwd_rbm.inc"
 
@@ -1208,8 +1252,11 @@ struct BwdArgs {
     const char* saved;
     char* ws;
     int64_t M, tiles;
-    const uint32_t* list;  // active tiles (tile_list_kernel) and their count
-    const uint32_t* count;
+    const uint32_t* list;       // segment lists of the active tiles (tile_flags_kernel)
+    const uint32_t* seg_count;
+    int64_t nseg;
+    uint32_t* dw_list;          // the dW kernel's list and count, built by workgroup 0
+    uint32_t* count;
     int L, Ld, n_layers;
     uint32_t skips;
     int slot_bytes;
@@ -1229,17 +1276,22 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     // wave -> entry blockIdx.x * (NT / 64) + wv of the active-tile list (one tile per wave);
     // waves past its end run on zero inputs and store nothing
     static_assert(TPW == 1, "the active-tile list gives each wave one tile");
-    const int64_t cnt = *a.count;
     const int64_t slot = static_cast<int64_t>(blockIdx.x) * (NT / 64) + wv;
-    if (static_cast<int64_t>(blockIdx.x) * (NT / 64) >= cnt) return;
-    const int64_t tile0 = slot < cnt ? static_cast<int64_t>(a.list[slot]) : 0;
+    // both scalar loads in flight together: past the count the list holds kTileNone
+    const uint32_t first = a.list[static_cast<int64_t>(blockIdx.x) * (NT / 64)], mine = a.list[slot];
+    if (first == kTileNone) {  // workgroup-uniform
+        if (blockIdx.x == 0)
+            build_tile_list(a.list, a.seg_count, a.nseg, a.dw_list, a.count, reinterpret_cast<uint32_t*>(lds));
+        return;
+    }
+    const int64_t tile0 = mine != kTileNone ? static_cast<int64_t>(mine) : 0;
     const int n = a.n_layers;
     const u32x4* masks = reinterpret_cast<const u32x4*>(a.saved + a.mask_off);
     bool tok[TPW];
     unsigned tokm = 0u;
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        tok[t] = slot + t < cnt;
+        tok[t] = mine != kTileNone;
         tokm |= (tok[t] ? 1u : 0u) << t;
     }
     // each dz image is saved while the next stream consumes it
@@ -1470,6 +1522,8 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
             }
         }
     }
+    if (blockIdx.x == 0)
+        build_tile_list(a.list, a.seg_count, a.nseg, a.dw_list, a.count, reinterpret_cast<uint32_t*>(lds));
 }
 
 // ------------------------------------------------ input gradients ------
@@ -1638,19 +1692,26 @@ __global__ __launch_bounds__(kDinNT) void mlp_dinput_kernel(DinArgs a) {
 // underflowed to 0 (the cumprod of 1 - alpha + 1e-10, rendering.py:87-96) receives
 // exactly zero g_rgb and g_sigma, so every layer's dz for it is zero.  A 32-sample
 // tile of such samples only adds exact zeros to dW, so the dX chain, the dW GEMM and
-// the input gradients run over the tiles with ANY nonzero incoming gradient.  The flag
-// is computed from the values (never assumed), in two launches: per-tile flags, then
-// one workgroup compacts them in tile order (deterministic list).
-constexpr int kTileFlagThreads = 256;  // 4 waves x 16 tiles per workgroup
-constexpr int kTilesPerFlagWg = 64;
-constexpr int kTileListThreads = 1024;
+// the input gradients run over the tiles with ANY nonzero incoming gradient (computed
+// from the values, never assumed).  One launch, no global scan: the tiles form
+// segments of kSegTiles; workgroup s writes segment s's flags, its active tiles in
+// tile order at seg_list[s * kSegTiles ...] (kTileNone past them) and their count.  The
+// dX kernels take a segment's entries eight (four) at a time; the dW kernel, which
+// splits the active tiles evenly over its chunks, scans the segment counts itself.
+// With every tile active, each kernel sees exactly the dense form's tiles in order.
+constexpr int kTileFlagThreads = 256;  // 4 waves x 16 tiles per workgroup = one segment
+static_assert(kSegTiles == 4 * 16, "one tile_flags_kernel workgroup per segment");
 
 __global__ __launch_bounds__(kTileFlagThreads) void tile_flags_kernel(const float* __restrict__ g_rgb,
                                                                       const float* __restrict__ g_sigma, int64_t M,
                                                                       int64_t tiles, int dense,
-                                                                      uint8_t* __restrict__ flags) {
-    const int lane = threadIdx.x & 63;
-    const int64_t tw = static_cast<int64_t>(blockIdx.x) * kTilesPerFlagWg + (threadIdx.x >> 6) * 16;
+                                                                      uint8_t* __restrict__ flags,
+                                                                      uint32_t* __restrict__ seg_list,
+                                                                      uint32_t* __restrict__ seg_count) {
+    __shared__ uint32_t wcnt[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t seg0 = static_cast<int64_t>(blockIdx.x) * kSegTiles;
+    const int64_t tw = seg0 + wv * 16;
     bool nz[8];
     // lanes 0-31: tile tw + 2 it, lanes 32-63: tile tw + 2 it + 1 (one sample each)
 #pragma unroll
@@ -1667,41 +1728,26 @@ __global__ __launch_bounds__(kTileFlagThreads) void tile_flags_kernel(const floa
         }
         nz[it] = v;
     }
+    uint32_t mask = 0;  // bit k: tile tw + k is active (wave-uniform)
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
         const uint64_t b = __ballot(nz[it]);
-        const int64_t t = tw + 2 * it + (lane >> 5);
-        if ((lane & 31) == 0 && t < tiles)
-            flags[t] = static_cast<uint8_t>(((lane >> 5) ? (b >> 32) : (b & 0xffffffffull)) != 0);
+        mask |= (static_cast<uint32_t>(b & 0xffffffffull) != 0 ? 1u : 0u) << (2 * it);
+        mask |= (static_cast<uint32_t>(b >> 32) != 0 ? 1u : 0u) << (2 * it + 1);
     }
-}
-
-// flags -> list of the active tiles in increasing order, and their count: thread i
-// counts its contiguous share of the flags, a workgroup scan gives its first slot.
-__global__ __launch_bounds__(kTileListThreads) void tile_list_kernel(const uint8_t* __restrict__ flags,
-                                                                     int64_t tiles, uint32_t* __restrict__ list,
-                                                                     uint32_t* __restrict__ count) {
-    __shared__ uint32_t part[kTileListThreads];
-    const int i = threadIdx.x;
-    const int64_t per = (tiles + kTileListThreads - 1) / kTileListThreads;
-    int64_t lo = i * per;
-    if (lo > tiles) lo = tiles;
-    int64_t hi = lo + per;
-    if (hi > tiles) hi = tiles;
-    uint32_t c = 0;
-    for (int64_t t = lo; t < hi; ++t) c += flags[t];
-    part[i] = c;
+    if (lane < 16 && tw + lane < tiles) flags[tw + lane] = static_cast<uint8_t>((mask >> lane) & 1u);
+    if (lane == 0) wcnt[wv] = __popc(mask);
     __syncthreads();
-    for (int off = 1; off < kTileListThreads; off <<= 1) {  // inclusive scan (Hillis-Steele)
-        const uint32_t v = i >= off ? part[i - off] : 0u;
-        __syncthreads();
-        part[i] += v;
-        __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        before += q < wv ? wcnt[q] : 0u;
+        total += wcnt[q];
     }
-    uint32_t slot = part[i] - c;
-    for (int64_t t = lo; t < hi; ++t)
-        if (flags[t]) list[slot++] = static_cast<uint32_t>(t);
-    if (i == kTileListThreads - 1) *count = part[i];
+    if (lane < 16 && ((mask >> lane) & 1u))
+        seg_list[seg0 + before + __popc(mask & ((1u << lane) - 1u))] = static_cast<uint32_t>(tw + lane);
+    if (threadIdx.x < kSegTiles && threadIdx.x >= total) seg_list[seg0 + threadIdx.x] = kTileNone;
+    if (threadIdx.x == 0) seg_count[blockIdx.x] = total;
 }
 
 // ------------------------------------------------------------------ dW ----
@@ -1732,8 +1778,9 @@ struct DwArgs {
     float* slabs;
     int njobs;
     int64_t tiles;
-    const uint32_t* list;           // active tiles (tile_list_kernel) and their count
+    const uint32_t* list;           // active tiles in order and their count (built during the dX launch)
     const uint32_t* count;
+    int list_lds;                   // LDS byte offset the chunk's list entries are staged to (0: read them global)
     int job_chunks[kMaxJobs];       // chunks of each job: list entries split evenly in order
     uint16_t wg_map[kDwMaxWgs];     // workgroup -> job | chunk << 5 (chunk-major: one chunk of every job in a row)
     int stage_bytes, nstage;
@@ -1872,11 +1919,20 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
             pdst[k] = pad ? -1 : pc * kFragBytes;
         }
     }
-    // stage list entry `pos` (tile list[pos], a scalar load) into buffer b
+    // this chunk's list entries, copied into LDS once when they fit (a scalar load per
+    // stage would wait on the L2 inside the tile loop: lgkmcnt also counts the transpose reads)
+    const uint32_t* lds_list = nullptr;
+    if (a.list_lds) {
+        uint32_t* dst = reinterpret_cast<uint32_t*>(lds + a.list_lds);
+        for (int64_t q = t0 + tid; q < t1; q += kDwThreads) dst[q - t0] = a.list[q];
+        __syncthreads();  // (before any staging DMA is in flight)
+        lds_list = dst;
+    }
+    // stage list entry `pos` into buffer b
     auto stage = [&](int b, int64_t pos) {
         char* dst = lds + b * a.stage_bytes;
         char* scratch = lds + a.nstage * a.stage_bytes;
-        const int64_t tile = a.list[pos];
+        const int64_t tile = lds_list ? lds_list[pos - t0] : a.list[pos];
 #pragma unroll
         for (int k = 0; k < kMaxPW; ++k) {
             if (k < per_wave) {
@@ -2903,16 +2959,17 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const MlpSizes z = make_sizes(p, M);
     NR_REQUIRE(z.tiles_alloc < (int64_t{1} << 32), "nr_mlp_backward_dx: M beyond 2^37 samples");
-    // the active-tile list (every tile with cfg->dense_backward)
+    // the segment lists of the active tiles (every tile with cfg->dense_backward); the dX
+    // launch's first workgroup concatenates them into the dW kernel's list
     char* wsb = static_cast<char*>(workspace);
     uint8_t* tflags = reinterpret_cast<uint8_t*>(wsb + z.flags_off);
-    uint32_t* tlist = reinterpret_cast<uint32_t*>(wsb + z.list_off);
+    uint32_t* seglist = reinterpret_cast<uint32_t*>(wsb + z.list_off + 0);
+    uint32_t* segcnt = reinterpret_cast<uint32_t*>(wsb + z.segcnt_off);
+    uint32_t* dwlist = reinterpret_cast<uint32_t*>(wsb + z.dwlist_off);
     uint32_t* tcount = reinterpret_cast<uint32_t*>(wsb + z.count_off);
-    hipLaunchKernelGGL(tile_flags_kernel, dim3(static_cast<unsigned>(ceil_div_ll(z.tiles, kTilesPerFlagWg))),
-                       dim3(kTileFlagThreads), 0, s, g_rgb, g_sigma, M, z.tiles, p.dense_bwd, tflags);
+    hipLaunchKernelGGL(tile_flags_kernel, dim3(static_cast<unsigned>(z.nseg)), dim3(kTileFlagThreads), 0, s, g_rgb,
+                       g_sigma, M, z.tiles, p.dense_bwd, tflags, seglist, segcnt);
     NR_LAUNCH_CHECK("nr_mlp_backward_dx (tile flags)");
-    hipLaunchKernelGGL(tile_list_kernel, dim3(1), dim3(kTileListThreads), 0, s, tflags, z.tiles, tlist, tcount);
-    NR_LAUNCH_CHECK("nr_mlp_backward_dx (tile list)");
     BwdArgs b;
     std::memset(&b, 0, sizeof(b));
     b.packed = static_cast<const char*>(packed);
@@ -2931,7 +2988,10 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     b.ws = static_cast<char*>(workspace);
     b.M = M;
     b.tiles = z.tiles;
-    b.list = tlist;
+    b.list = seglist;
+    b.seg_count = segcnt;
+    b.nseg = z.nseg;
+    b.dw_list = dwlist;
     b.count = tcount;
     b.L = p.L;
     b.Ld = p.Ld;
@@ -2977,7 +3037,10 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
         r.ws = b.ws;
         r.M = M;
         r.tiles = z.tiles;
-        r.list = tlist;
+        r.list = seglist;
+        r.seg_count = segcnt;
+        r.nseg = z.nseg;
+        r.dw_list = dwlist;
         r.count = tcount;
         r.scratch_tile = z.tiles_alloc - 1;
         r.n_layers = n;
@@ -3033,7 +3096,7 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
     std::memset(&w, 0, sizeof(w));
     w.slabs = reinterpret_cast<float*>(ws + z.slab_off);
     w.tiles = z.tiles;
-    w.list = reinterpret_cast<const uint32_t*>(ws + z.list_off);  // written by nr_mlp_backward_dx
+    w.list = reinterpret_cast<const uint32_t*>(ws + z.dwlist_off);  // written by nr_mlp_backward_dx
     w.count = reinterpret_cast<const uint32_t*>(ws + z.count_off);
     w.njobs = p.n_jobs;
     int nwg = 0;
@@ -3082,7 +3145,15 @@ int nr_mlp_backward_dw(const NrMlpConfig* cfg, int64_t M, const void* saved, voi
     // as many stages as fit in 160 KiB (+1 KB scratch): 4 for bf16, 2 for fp32
     w.nstage = static_cast<int>((160 * 1024 - kFragBytes) / w.stage_bytes);
     if (w.nstage > NR_DW_NSTAGE) w.nstage = NR_DW_NSTAGE;
-    const size_t lds = static_cast<size_t>(w.nstage) * w.stage_bytes + kFragBytes;
+    size_t lds = static_cast<size_t>(w.nstage) * w.stage_bytes + kFragBytes;
+    // the largest chunk's list entries behind the stages, when they fit
+    int min_chunks = z.job_chunks[0];
+    for (int j = 1; j < p.n_jobs; ++j) min_chunks = z.job_chunks[j] < min_chunks ? z.job_chunks[j] : min_chunks;
+    const size_t list_bytes = (static_cast<size_t>(ceil_div_ll(z.tiles, min_chunks)) * 4 + 15) / 16 * 16;
+    if (lds + list_bytes <= 160 * 1024) {
+        w.list_lds = static_cast<int>(lds);
+        lds += list_bytes;
+    }
     NR_REQUIRE(w.nstage >= 2, "nr_mlp_backward_dw: a %d-byte stage does not fit twice in LDS", w.stage_bytes);
     NR_REQUIRE(lds <= 160 * 1024, "nr_mlp_backward_dw: %zu bytes of LDS staging exceeds 160 KiB", lds);
     const dim3 grid(static_cast<unsigned>(nwg)), block(kDwThreads);

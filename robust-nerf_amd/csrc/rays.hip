@@ -23,10 +23,6 @@ __device__ __forceinline__ float linspace_at(float start, float end, int n, int 
                        : end - step * static_cast<float>(n - 1 - i);
 }
 
-__device__ __forceinline__ float norm3(float x, float y, float z) {
-    return sqrtf(x * x + y * y + z * z);
-}
-
 // ---------------------------------------------------------------- A1 -----
 __global__ void ray_directions_kernel(int H, int W, float focal, float cx, float cy, float* dirs) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -382,7 +378,7 @@ __global__ void gather_rays_kernel(const int64_t* idx, int64_t n_rays, int B, co
 
 // ---------------------------------------------------------------- A5 -----
 __global__ void stratified_kernel(const float* ro, const float* rd, const float* t_rand, float near_,
-                                  float far_, int lindisp, int B, int N, float* z_out, float* pts) {
+                                  float far_, int lindisp, int B, int N, float* z_out, float* pts, float* vd) {
     const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (p >= static_cast<int64_t>(B) * N) return;
     const int b = static_cast<int>(p / N), i = static_cast<int>(p % N);
@@ -402,6 +398,13 @@ __global__ void stratified_kernel(const float* ro, const float* rd, const float*
     z_out[p] = z;
     if (pts) {
         for (int c = 0; c < 3; ++c) pts[3 * p + c] = ro[3 * b + c] + rd[3 * b + c] * z;
+    }
+    if (vd) {  // rendering.py:165, broadcast to the samples (expand_viewdirs_kernel's values)
+        const float x = rd[3 * b], y = rd[3 * b + 1], w = rd[3 * b + 2];
+        const float n = norm3(x, y, w);
+        vd[3 * p] = x / n;
+        vd[3 * p + 1] = y / n;
+        vd[3 * p + 2] = w / n;
     }
 }
 
@@ -618,12 +621,13 @@ int nr_gather_rays(const int64_t* idx, int64_t n_rays, int B, const float* rays_
 }
 
 int nr_stratified_sample(const float* ro, const float* rd, const float* t_rand, float near_, float far_,
-                         int lindisp, int B, int N, float* z, float* pts, nr_stream_t stream) {
-    NR_REQUIRE(z && B >= 0 && N > 0 && (!pts || (ro && rd)), "nr_stratified_sample: bad arguments");
+                         int lindisp, int B, int N, float* z, float* pts, float* viewdirs, nr_stream_t stream) {
+    NR_REQUIRE(z && B >= 0 && N > 0 && (!pts || (ro && rd)) && (!viewdirs || rd),
+               "nr_stratified_sample: bad arguments");
     const int64_t n = static_cast<int64_t>(B) * N;
     if (n == 0) return NR_OK;
     hipLaunchKernelGGL(stratified_kernel, dim3(static_cast<unsigned>(ceil_div_ll(n, 256))), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), ro, rd, t_rand, near_, far_, lindisp, B, N, z, pts);
+                       static_cast<hipStream_t>(stream), ro, rd, t_rand, near_, far_, lindisp, B, N, z, pts, viewdirs);
     NR_LAUNCH_CHECK("nr_stratified_sample");
     return NR_OK;
 }

@@ -104,7 +104,8 @@ __global__ void sample_pdf_kernel(const float* bins_g, const float* w_g, const f
 }
 
 __global__ void sample_hier_kernel(const float* ro, const float* rd, const float* zc_g, const float* wc_g,
-                                   const float* u_g, int B, int Nc, int Nf, float* zf_out, float* pts_out) {
+                                   const float* u_g, int B, int Nc, int Nf, float* zf_out, float* pts_out,
+                                   float* vd_out) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int b = blockIdx.x * kRaysPerBlock + wv;
@@ -157,9 +158,14 @@ __global__ void sample_hier_kernel(const float* ro, const float* rd, const float
     }
     const int64_t ob = static_cast<int64_t>(b) * T;
     float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 0.f, dz = 0.f;
-    if (pts_out) {
-        ox = ro[3 * b], oy = ro[3 * b + 1], oz = ro[3 * b + 2];
+    if (pts_out || vd_out) {
+        ox = ro ? ro[3 * b] : 0.f, oy = ro ? ro[3 * b + 1] : 0.f, oz = ro ? ro[3 * b + 2] : 0.f;
         dx = rd[3 * b], dy = rd[3 * b + 1], dz = rd[3 * b + 2];
+    }
+    float vx = 0.f, vy = 0.f, vz = 0.f;
+    if (vd_out) {  // rendering.py:165 (expand_viewdirs_kernel's values)
+        const float dn = norm3(dx, dy, dz);
+        vx = dx / dn, vy = dy / dn, vz = dz / dn;
     }
     for (int e = lane; e < T; e += 64) {
         const float v = uni[e];
@@ -169,6 +175,11 @@ __global__ void sample_hier_kernel(const float* ro, const float* rd, const float
             pts_out[3 * o] = ox + dx * v;
             pts_out[3 * o + 1] = oy + dy * v;
             pts_out[3 * o + 2] = oz + dz * v;
+        }
+        if (vd_out) {
+            vd_out[3 * o] = vx;
+            vd_out[3 * o + 1] = vy;
+            vd_out[3 * o + 2] = vz;
         }
     }
 }
@@ -192,8 +203,8 @@ int nr_sample_pdf(const float* bins, const float* weights, const float* u, int B
 }
 
 int nr_sample_hierarchical(const float* ro, const float* rd, const float* zc, const float* wc, const float* u,
-                           int B, int Nc, int Nf, float* zf, float* pts, nr_stream_t stream) {
-    NR_REQUIRE(zc && wc && zf && B >= 0 && Nc >= 3 && Nf > 0 && (!pts || (ro && rd)),
+                           int B, int Nc, int Nf, float* zf, float* pts, float* viewdirs, nr_stream_t stream) {
+    NR_REQUIRE(zc && wc && zf && B >= 0 && Nc >= 3 && Nf > 0 && (!pts || (ro && rd)) && (!viewdirs || rd),
                "nr_sample_hierarchical: bad arguments");
     NR_REQUIRE(Nc + Nf <= 64 * kMaxPerLane, "nr_sample_hierarchical: Nc+Nf=%d exceeds %d", Nc + Nf,
                64 * kMaxPerLane);
@@ -203,7 +214,7 @@ int nr_sample_hierarchical(const float* ro, const float* rd, const float* zc, co
     const size_t lds = sizeof(float) * kRaysPerBlock * (3 * (Nc - 1) + P2);
     const dim3 grid(ceil_div(B, kRaysPerBlock)), block(64 * kRaysPerBlock);
     const hipStream_t st = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(sample_hier_kernel, grid, block, lds, st, ro, rd, zc, wc, u, B, Nc, Nf, zf, pts);
+    hipLaunchKernelGGL(sample_hier_kernel, grid, block, lds, st, ro, rd, zc, wc, u, B, Nc, Nf, zf, pts, viewdirs);
     NR_LAUNCH_CHECK("nr_sample_hierarchical");
     return NR_OK;
 }

@@ -81,11 +81,11 @@ _SIGNATURES = {
     "nr_check_index_range": (c_i, [c_vp, c_i, c_i, c_vp, c_vp]),
     "nr_se3_poses_bwd": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_vp, c_i, c_vp, c_vp, c_vp]),
     "nr_gather_rays": (c_i, [c_vp, c_i64, c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "nr_stratified_sample": (c_i, [c_vp, c_vp, c_vp, c_f, c_f, c_i, c_i, c_i, c_vp, c_vp, c_vp]),
+    "nr_stratified_sample": (c_i, [c_vp, c_vp, c_vp, c_f, c_f, c_i, c_i, c_i, c_vp, c_vp, c_vp, c_vp]),
     "nr_positional_encoding": (c_i, [c_vp, c_i64, c_i, c_i, c_i, c_i, c_vp, c_vp]),
     "nr_positional_encoding_bwd": (c_i, [c_vp, c_i64, c_i, c_i, c_i, c_i, c_vp, c_vp, c_vp]),
     "nr_sample_pdf": (c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_i, c_vp, c_vp]),
-    "nr_sample_hierarchical": (c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_vp, c_vp, c_vp]),
+    "nr_sample_hierarchical": (c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_vp, c_vp, c_vp, c_vp]),
     "nr_composite_fwd": (c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "nr_composite_bwd": (c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_vp, c_vp, c_vp, c_vp,
                                c_vp, c_vp, c_vp, c_vp]),
@@ -112,6 +112,9 @@ _SIGNATURES = {
     "nr_expand_viewdirs": (c_i, [c_vp, c_i, c_i, c_vp, c_vp]),
     "nr_pts_bwd": (c_i, [c_vp, c_vp, c_i, c_i, c_vp, c_vp, c_vp]),
     "nr_viewdirs_bwd": (c_i, [c_vp, c_vp, c_i, c_i, c_vp, c_vp]),
+    "nr_composite_mse_workspace_bytes": (c_i64, [c_i]),
+    "nr_composite_mse": (c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_f, c_vp, c_vp, c_vp, c_vp, c_vp,
+                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "nr_mse_fwd_bwd": (c_i, [c_vp, c_vp, c_i, c_f, c_vp, c_vp, c_vp]),
 }
 

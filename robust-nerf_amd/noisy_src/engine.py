@@ -245,30 +245,29 @@ class Trainer:
         early = {}
 
         def coarse_backward(out_c):
-            # on the coarse stream: the coarse loss and its backward, beside the fine
-            # forward (loss = loss_c + loss_f sends exactly d loss_c to the coarse net);
-            # target_rgb may come from the current stream's pool (record_stream: see
-            # render_rays)
-            target_rgb.record_stream(torch.cuda.current_stream(target_rgb.device))
-            early["loss_c"] = ops.mse_loss(out_c["rgb_map"], target_rgb, gs)
+            # on the coarse stream: the coarse loss's backward, beside the fine forward
+            # (loss = loss_c + loss_f sends exactly d loss_c to the coarse net)
+            early["loss_c"] = out_c["loss"]
             early["loss_c"].backward(ops.unit_grad(rays_o.device))
 
+        # the MSE losses (train.py:89/98) come out of the compositing (ops.composite_mse)
         out = render_rays(self.model_coarse, self.model_fine, rays_o, rays_d, self.render_config, is_train=True,
                           t_rand=t_rand, u=u, coarse_stream=cs,
-                          coarse_backward=coarse_backward if cs is not None else None)
+                          coarse_backward=coarse_backward if cs is not None else None,
+                          target_rgb=target_rgb, loss_scale=gs)
         if cs is not None:
-            loss_f = ops.mse_loss(out["rgb_fine"], target_rgb, gs)
+            loss_f = out["loss_fine"]
             loss_f.backward(ops.unit_grad(rays_o.device))
             torch.cuda.current_stream(rays_o.device).wait_stream(cs)  # join the coarse chain
             loss_c = early["loss_c"].detach()
             loss = loss_c + loss_f.detach()  # the backward already ran: the value only
             metrics = {"loss_coarse": loss_c.detach(), "loss_fine": loss_f.detach()}
         else:
-            loss_c = ops.mse_loss(out["rgb_coarse"], target_rgb, gs)
+            loss_c = out["loss_coarse"]
             loss = loss_c
             metrics = {"loss_coarse": loss_c.detach()}  # metrics hold no autograd graph
-            if "rgb_fine" in out:
-                loss_f = ops.mse_loss(out["rgb_fine"], target_rgb, gs)
+            if "loss_fine" in out:
+                loss_f = out["loss_fine"]
                 loss = loss_c + loss_f
                 metrics["loss_fine"] = loss_f.detach()
             loss.backward(ops.unit_grad(loss.device))
@@ -483,14 +482,15 @@ class PoseTrainer:
             poses = poses.detach()
         rays_o, rays_d = self.pixel_sampler.get_rays_for_batch(pixel_batch, poses)
         target = pixel_batch.target_rgb
-        out = render_rays(self.model_coarse, self.model_fine, rays_o, rays_d, self.render_config, is_train=True,
-                          t_rand=t_rand, u=u)
         gs = self.reducer.prescale if self.reducer is not None else 1.0  # DP: 1/world in the seed
-        loss_c = ops.mse_loss(out["rgb_coarse"], target, gs)
+        # the MSE losses (train_pose_opt.py:355-370) come out of the compositing
+        out = render_rays(self.model_coarse, self.model_fine, rays_o, rays_d, self.render_config, is_train=True,
+                          t_rand=t_rand, u=u, target_rgb=target, loss_scale=gs)
+        loss_c = out["loss_coarse"]
         loss = loss_c
         metrics = {"loss_coarse": loss_c.detach()}  # metrics hold no autograd graph
-        if "rgb_fine" in out:
-            loss_f = ops.mse_loss(out["rgb_fine"], target, gs)
+        if "loss_fine" in out:
+            loss_f = out["loss_fine"]
             loss = loss_c + loss_f
             metrics["loss_fine"] = loss_f.detach()
         bwd = loss

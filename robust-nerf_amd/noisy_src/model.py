@@ -212,6 +212,18 @@ class NeRF(nn.Module):
         self._grad_ready_hook = None
         # a list: every backward appends (M, its device count of active 32-sample tiles)
         self._tile_counts: Optional[list] = None
+        self._tickets = {}  # device -> the persistent zeroed word of loss_ticket
+
+    def loss_ticket(self, device) -> torch.Tensor:
+        """A persistent device word, zero between launches, that the fused composite + MSE
+        launch of this network's samples uses to sum its loss in the launch
+        (ops.composite_mse).  One per network: the coarse and fine chains may run
+        concurrently, each with its own."""
+        t = self._tickets.get(device)
+        if t is None:
+            t = torch.zeros(4, device=device, dtype=torch.int32)
+            self._tickets[device] = t
+        return t
 
     # -- flat parameter buffer -------------------------------------------------
     @property

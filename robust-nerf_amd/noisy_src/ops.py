@@ -116,32 +116,45 @@ def _pts_bwd(ctx, g_pts, z):
     return g_o, g_d
 
 
+def _viewdirs_bwd(ctx, g_vd, rd, S, g_d):
+    """viewdirs = rays_d / |rays_d| per sample (rendering.py:165): accumulate into g_d."""
+    if g_vd is None or not ctx.needs_input_grad[1]:
+        return g_d
+    if g_d is None:
+        g_d = torch.zeros_like(rd)
+    call("nr_viewdirs_bwd", ptr(rd), ptr(_c(g_vd)), rd.shape[0], S, ptr(g_d), _stream())
+    return g_d
+
+
 class _Stratified(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, rays_o, rays_d, t_rand, near, far, lindisp, num_samples):
+    def forward(ctx, rays_o, rays_d, t_rand, near, far, lindisp, num_samples, with_vd):
         ro, rd = _c(rays_o), _c(rays_d)
         B = ro.shape[0]
         z = torch.empty(B, num_samples, device=ro.device, dtype=_f32)
         pts = torch.empty(B, num_samples, 3, device=ro.device, dtype=_f32)
+        vd = torch.empty(B * num_samples, 3, device=ro.device, dtype=_f32) if with_vd else None
         tr = _c(t_rand)
         call("nr_stratified_sample", ptr(ro), ptr(rd), ptr(tr), float(near), float(far), int(bool(lindisp)), B,
-             num_samples, ptr(z), ptr(pts), _stream())
-        ctx.save_for_backward(z)
+             num_samples, ptr(z), ptr(pts), ptr(vd), _stream())
+        ctx.save_for_backward(z, rd)
         ctx.mark_non_differentiable(z)
         ctx.set_materialize_grads(False)  # no zero-filled dL/dz launch per step
-        return pts, z
+        return (pts, z, vd) if with_vd else (pts, z)
 
     @staticmethod
-    def backward(ctx, g_pts, _g_z):
-        (z,) = ctx.saved_tensors
+    def backward(ctx, g_pts, _g_z, g_vd=None):
+        z, rd = ctx.saved_tensors
         g_o, g_d = _pts_bwd(ctx, g_pts, z)
-        return g_o, g_d, None, None, None, None, None
+        g_d = _viewdirs_bwd(ctx, g_vd, rd, z.shape[1], g_d)
+        return g_o, g_d, None, None, None, None, None, None
 
 
-def stratified_sample(rays_o, rays_d, near, far, num_samples, t_rand=None, lindisp=False):
-    """Returns (pts (B,N,3), z (B,N)); t_rand None -> no perturbation."""
+def stratified_sample(rays_o, rays_d, near, far, num_samples, t_rand=None, lindisp=False, viewdirs=False):
+    """Returns (pts (B,N,3), z (B,N)) -- and with ``viewdirs`` the normalised directions
+    per sample (B*N,3) from the same launch; t_rand None -> no perturbation."""
     _check(rays_o, rays_d, t_rand)
-    return _Stratified.apply(rays_o, rays_d, t_rand, near, far, lindisp, num_samples)
+    return _Stratified.apply(rays_o, rays_d, t_rand, near, far, lindisp, num_samples, bool(viewdirs))
 
 
 def sample_pdf(bins, weights, num_samples, u=None):
@@ -158,34 +171,37 @@ def sample_pdf(bins, weights, num_samples, u=None):
 
 class _Hierarchical(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, rays_o, rays_d, z_coarse, w_coarse, u, num_samples_fine):
+    def forward(ctx, rays_o, rays_d, z_coarse, w_coarse, u, num_samples_fine, with_vd):
         ro, rd = _c(rays_o), _c(rays_d)
         zc, wc = _c(z_coarse), _c(w_coarse)
         B, Nc = zc.shape
         T = Nc + num_samples_fine
         zf = torch.empty(B, T, device=zc.device, dtype=_f32)
         pts = torch.empty(B, T, 3, device=zc.device, dtype=_f32)
+        vd = torch.empty(B * T, 3, device=zc.device, dtype=_f32) if with_vd else None
         uu = _c(u)
         call("nr_sample_hierarchical", ptr(ro), ptr(rd), ptr(zc), ptr(wc), ptr(uu), B, Nc, num_samples_fine,
-             ptr(zf), ptr(pts), _stream())
-        ctx.save_for_backward(zf)
+             ptr(zf), ptr(pts), ptr(vd), _stream())
+        ctx.save_for_backward(zf, rd)
         ctx.mark_non_differentiable(zf)
         ctx.set_materialize_grads(False)
-        return pts, zf
+        return (pts, zf, vd) if with_vd else (pts, zf)
 
     @staticmethod
-    def backward(ctx, g_pts, _g_z):
-        (zf,) = ctx.saved_tensors
+    def backward(ctx, g_pts, _g_z, g_vd=None):
+        zf, rd = ctx.saved_tensors
         g_o, g_d = _pts_bwd(ctx, g_pts, zf)
-        return g_o, g_d, None, None, None, None
+        g_d = _viewdirs_bwd(ctx, g_vd, rd, zf.shape[1], g_d)
+        return g_o, g_d, None, None, None, None, None
 
 
-def sample_hierarchical(rays_o, rays_d, z_coarse, w_coarse, num_samples_fine, u=None):
-    """Returns (pts_fine (B,Nc+Nf,3), z_fine (B,Nc+Nf)); u None -> det.  The fine
+def sample_hierarchical(rays_o, rays_d, z_coarse, w_coarse, num_samples_fine, u=None, viewdirs=False):
+    """Returns (pts_fine (B,Nc+Nf,3), z_fine (B,Nc+Nf)) -- and with ``viewdirs`` the
+    normalised directions per sample from the same launch; u None -> det.  The fine
     depths are detached as in the reference (rays.py:325)."""
     _check(rays_o, rays_d, z_coarse, w_coarse, u)
     return _Hierarchical.apply(rays_o, rays_d, z_coarse.detach(), w_coarse.detach(),
-                               u.detach() if u is not None else None, num_samples_fine)
+                               u.detach() if u is not None else None, num_samples_fine, bool(viewdirs))
 
 
 # ---------------------------------------------------------------- viewdirs ---
@@ -284,6 +300,70 @@ def composite(rgb, sigma, z_vals, rays_d, noise=None, white_background=True):
     _check(rgb, sigma, z_vals, rays_d, noise)
     sig = sigma.reshape(z_vals.shape)
     return _Composite.apply(rgb, sig, z_vals, rays_d, noise, bool(white_background))
+
+
+class _CompositeMSE(torch.autograd.Function):
+    """raw2outputs + mean((rgb_map - target)^2) of one training step, one launch pair
+    (nr_composite_mse): the forward also produces the gradient of ``grad_scale * loss``
+    w.r.t. rgb / sigma (/ rays_d), which the backward hands over (bit-identical to the
+    composite forward, MSE and composite backward run separately).  Gradients arriving
+    at rgb_map / depth / acc / weights from elsewhere add a composite backward of their own."""
+
+    @staticmethod
+    def forward(ctx, rgb, sigma, z, rays_d, noise, target, white, grad_scale, ticket):
+        rgb, sigma, z, rd, tgt = _c(rgb), _c(sigma), _c(z), _c(rays_d), _c(target)
+        B, S = z.shape
+        nz = _c(noise)
+        dev = z.device
+        rgb_map = torch.empty(B, 3, device=dev, dtype=_f32)
+        depth = torch.empty(B, device=dev, dtype=_f32)
+        acc = torch.empty(B, device=dev, dtype=_f32)
+        weights = torch.empty(B, S, device=dev, dtype=_f32)
+        loss = torch.empty((), device=dev, dtype=_f32)
+        g_rgb = torch.empty_like(rgb)
+        g_sigma = torch.empty(B, S, device=dev, dtype=_f32)
+        g_rd = torch.zeros_like(rd) if ctx.needs_input_grad[3] else None
+        ws = torch.empty(max(16, int(_hip.load().nr_composite_mse_workspace_bytes(B))), device=dev, dtype=torch.uint8)
+        call("nr_composite_mse", ptr(rgb), ptr(sigma), ptr(z), ptr(rd), ptr(nz), ptr(tgt), B, S, int(white),
+             float(grad_scale), ptr(rgb_map), ptr(depth), ptr(acc), ptr(weights), ptr(loss), ptr(g_rgb), ptr(g_sigma),
+             ptr(g_rd), ptr(ticket), ptr(ws), _stream())
+        ctx.save_for_backward(rgb, sigma, z, rd, nz, g_rgb, g_sigma, g_rd)
+        ctx.white = white
+        ctx.sigma_shape = sigma.shape
+        ctx.set_materialize_grads(False)
+        return loss, rgb_map, depth, acc, weights
+
+    @staticmethod
+    def backward(ctx, g_loss, g_map, g_depth, g_acc, g_w):
+        rgb, sigma, z, rd, nz, g_rgb, g_sigma, g_rd = ctx.saved_tensors
+        B, S = z.shape
+        if g_loss is None:
+            g_rgb, g_sigma = torch.zeros_like(g_rgb), torch.zeros_like(g_sigma)
+            g_rd = torch.zeros_like(g_rd) if g_rd is not None else None
+        elif g_loss.data_ptr() != _unit.get(g_loss.device, _NO_UNIT).data_ptr():
+            g_rgb, g_sigma = g_rgb * g_loss, g_sigma * g_loss
+            g_rd = g_rd * g_loss if g_rd is not None else None
+        if any(t is not None for t in (g_map, g_depth, g_acc, g_w)):
+            e_rgb, e_sigma = torch.empty_like(rgb), torch.empty(B, S, device=z.device, dtype=_f32)
+            e_rd = torch.zeros_like(rd) if g_rd is not None else None
+            gm = _c(g_map) if g_map is not None else torch.zeros(B, 3, device=z.device, dtype=_f32)
+            call("nr_composite_bwd", ptr(rgb), ptr(sigma), ptr(z), ptr(rd), ptr(nz), B, S, int(ctx.white), ptr(gm),
+                 ptr(_c(g_depth)), ptr(_c(g_acc)), ptr(_c(g_w)), ptr(e_rgb), ptr(e_sigma), ptr(e_rd), _stream())
+            g_rgb, g_sigma = g_rgb + e_rgb, g_sigma + e_sigma
+            g_rd = g_rd + e_rd if g_rd is not None else None
+        return g_rgb, g_sigma.view(ctx.sigma_shape), None, g_rd, None, None, None, None, None
+
+
+def composite_mse(rgb, sigma, z_vals, rays_d, target, noise=None, white_background=True, grad_scale=1.0,
+                  ticket=None):
+    """Training form of raw2outputs + the MSE loss against ``target`` (B,3): returns
+    (loss, rgb_map, depth, acc, weights); the loss's gradient carries ``grad_scale``.
+    ``ticket``: a persistent zeroed int32 device word (NeRF.loss_ticket) that lets the
+    launch sum the loss itself; calls sharing it must not run concurrently."""
+    _check(rgb, sigma, z_vals, rays_d, target, noise, ticket)
+    sig = sigma.reshape(z_vals.shape)
+    return _CompositeMSE.apply(rgb, sig, z_vals, rays_d, noise, target, bool(white_background), float(grad_scale),
+                               ticket)
 
 
 # ---------------------------------------------------------------- A3 / A4 ----

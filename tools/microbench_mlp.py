@@ -2,6 +2,7 @@
 import ctypes, sys, torch
 sys.path[:0] = [".", "robust-nerf_amd"]
 from noisy_src import _hip
+_hip.load(require_all=False)  # NR_HIP_LIB may name an older library (A/B runs)
 from noisy_src.config import ModelConfig
 from noisy_src.model import NeRF
 MACS = 593408
