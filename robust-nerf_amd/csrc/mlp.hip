@@ -1189,48 +1189,23 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     }
 }
 
-// The dW kernel's work list, built by the FIRST workgroup of the dX launch after its own
-// tiles (off the critical path: the other workgroups keep the GPU busy): the segment
-// lists of tile_flags_kernel concatenated in segment order -- every active tile once, in
-// increasing order -- and their total.  sh: LDS scratch of 2 * blockDim.x + 16 words.
-__device__ void build_tile_list(const uint32_t* __restrict__ seg_list, const uint32_t* __restrict__ seg_count,
-                                int64_t nseg, uint32_t* __restrict__ list, uint32_t* __restrict__ count,
-                                uint32_t* sh) {
-    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
-    uint32_t* wsum = sh;           // [16]
-    uint32_t* starts = sh + 16;    // [nt]
-    uint32_t* cnts = starts + nt;  // [nt]
-    __syncthreads();
-    uint32_t base = 0;
-    for (int64_t s0 = 0; s0 < nseg; s0 += nt) {
-        const int64_t sg = s0 + tid;
-        const uint32_t c = sg < nseg ? seg_count[sg] : 0u;
-        uint32_t incl = c;
+// The dW kernel's work list: the segment lists of tile_flags_kernel concatenated in
+// segment order (every active tile once, in increasing order) and their total.  Each
+// segment's entries are placed by wave 0 of the dX workgroup that leads the segment (the
+// first of its kSegTiles / waves-per-workgroup workgroups), after its own tiles: it sums
+// the counts of the segments before it (independent loads, one wave reduction) and
+// copies the segment's entries with one coalesced load and store.
+__device__ __forceinline__ void place_segment(const uint32_t* __restrict__ seg_list,
+                                              const uint32_t* __restrict__ seg_count, int64_t nseg, int64_t sg,
+                                              uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
+    const int lane = threadIdx.x & 63;
+    uint32_t before = 0;
+    for (int64_t q = lane; q < sg; q += 64) before += seg_count[q];
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(incl, d);
-            if (lane >= d) incl += o;
-        }
-        if (lane == 63) wsum[wv] = incl;
-        __syncthreads();
-        uint32_t before = 0, total = 0;
-        for (int q = 0; q < nw; ++q) {
-            const uint32_t v = wsum[q];
-            before += q < wv ? v : 0u;
-            total += v;
-        }
-        starts[tid] = base + before + incl - c;
-        cnts[tid] = c;
-        __syncthreads();
-        // one wave per segment: lane l copies entry l (coalesced)
-        const int nj = static_cast<int>(nseg - s0 < nt ? nseg - s0 : nt);
-        for (int j = wv; j < nj; j += nw) {
-            if (static_cast<uint32_t>(lane) < cnts[j]) list[starts[j] + lane] = seg_list[(s0 + j) * kSegTiles + lane];
-        }
-        base += total;
-        __syncthreads();
-    }
-    if (tid == 0) *count = base;
+    for (int d = 32; d > 0; d >>= 1) before += __shfl_xor(before, d);
+    const uint32_t c = seg_count[sg];
+    if (static_cast<uint32_t>(lane) < c) list[before + lane] = seg_list[sg * kSegTiles + lane];
+    if (sg == nseg - 1 && lane == 0) *count = before + c;
 }
 
 #include "mlp_fwd_rbm.inc"
@@ -1255,7 +1230,7 @@ struct BwdArgs {
     const uint32_t* list;       // segment lists of the active tiles (tile_flags_kernel)
     const uint32_t* seg_count;
     int64_t nseg;
-    uint32_t* dw_list;          // the dW kernel's list and count, built by workgroup 0
+    uint32_t* dw_list;          // the dW kernel's list and count (place_segment)
     uint32_t* count;
     int L, Ld, n_layers;
     uint32_t skips;
@@ -1273,15 +1248,19 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ml = lane & 31;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // wave -> entry blockIdx.x * (NT / 64) + wv of the active-tile list (one tile per wave);
-    // waves past its end run on zero inputs and store nothing
+    // workgroup -> (segment, part j): segment-minor, so the active parts (small j) are
+    // the first workgroups dispatched and spread over every XCD; wave -> entry
+    // j * (NT / 64) + wv of the segment's list (one tile per wave); waves past its count
+    // run on zero inputs and store nothing
     static_assert(TPW == 1, "the active-tile list gives each wave one tile");
-    const int64_t slot = static_cast<int64_t>(blockIdx.x) * (NT / 64) + wv;
-    // both scalar loads in flight together: past the count the list holds kTileNone
-    const uint32_t first = a.list[static_cast<int64_t>(blockIdx.x) * (NT / 64)], mine = a.list[slot];
+    const int64_t my_seg = blockIdx.x % a.nseg;
+    const int part = static_cast<int>(blockIdx.x / a.nseg);
+    const int64_t first_slot = my_seg * kSegTiles + part * (NT / 64), slot = first_slot + wv;
+    // both scalar loads in flight together: past the segment's count the list holds kTileNone
+    const uint32_t first = a.list[first_slot], mine = a.list[slot];
+    const bool leader = part == 0 && wv == 0;  // wave 0 of a segment's first workgroup
     if (first == kTileNone) {  // workgroup-uniform
-        if (blockIdx.x == 0)
-            build_tile_list(a.list, a.seg_count, a.nseg, a.dw_list, a.count, reinterpret_cast<uint32_t*>(lds));
+        if (leader) place_segment(a.list, a.seg_count, a.nseg, my_seg, a.dw_list, a.count);
         return;
     }
     const int64_t tile0 = mine != kTileNone ? static_cast<int64_t>(mine) : 0;
@@ -1522,8 +1501,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
             }
         }
     }
-    if (blockIdx.x == 0)
-        build_tile_list(a.list, a.seg_count, a.nseg, a.dw_list, a.count, reinterpret_cast<uint32_t*>(lds));
+    if (leader) place_segment(a.list, a.seg_count, a.nseg, my_seg, a.dw_list, a.count);
 }
 
 // ------------------------------------------------ input gradients ------
@@ -1696,9 +1674,10 @@ __global__ __launch_bounds__(kDinNT) void mlp_dinput_kernel(DinArgs a) {
 // from the values, never assumed).  One launch, no global scan: the tiles form
 // segments of kSegTiles; workgroup s writes segment s's flags, its active tiles in
 // tile order at seg_list[s * kSegTiles ...] (kTileNone past them) and their count.  The
-// dX kernels take a segment's entries eight (four) at a time; the dW kernel, which
-// splits the active tiles evenly over its chunks, scans the segment counts itself.
-// With every tile active, each kernel sees exactly the dense form's tiles in order.
+// dX kernels take a segment's entries eight (four) at a time and concatenate the
+// segments into the dW kernel's list (place_segment), which that kernel splits evenly over
+// its chunks.  With every tile active, each kernel sees exactly the dense form's tiles in
+// order.
 constexpr int kTileFlagThreads = 256;  // 4 waves x 16 tiles per workgroup = one segment
 static_assert(kSegTiles == 4 * 16, "one tile_flags_kernel workgroup per segment");
 
@@ -1922,17 +1901,32 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
     // this chunk's list entries, copied into LDS once when they fit (a scalar load per
     // stage would wait on the L2 inside the tile loop: lgkmcnt also counts the transpose reads)
     const uint32_t* lds_list = nullptr;
-    if (a.list_lds) {
+    if (a.list_lds && cnt != a.tiles) {  // (every tile active: the list is the identity)
         uint32_t* dst = reinterpret_cast<uint32_t*>(lds + a.list_lds);
         for (int64_t q = t0 + tid; q < t1; q += kDwThreads) dst[q - t0] = a.list[q];
         __syncthreads();  // (before any staging DMA is in flight)
         lds_list = dst;
     }
-    // stage list entry `pos` into buffer b
-    auto stage = [&](int b, int64_t pos) {
+    // the tile of list entry pos: with every tile active the list is the identity (no read:
+    // the dense form's cost); else from the LDS copy through asm with its own wait (a
+    // compiler-visible LDS load behind the staging DMA makes hipcc wait vmcnt(0) for the
+    // DMA, which writes LDS), or from the global list when the copy did not fit
+    const bool ident = cnt == a.tiles;
+    const uint32_t list_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds_list));
+    auto tile_at = [&](int64_t pos) -> int64_t {
+        if (ident) return pos;
+        if (!lds_list) return a.list[pos];
+        uint32_t v;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(v)
+                     : "v"(list_base + 4u * static_cast<uint32_t>(pos - t0))
+                     : "memory");
+        return __builtin_amdgcn_readfirstlane(v);
+    };
+    // stage `tile` into buffer b
+    auto stage = [&](int b, int64_t tile) {
         char* dst = lds + b * a.stage_bytes;
         char* scratch = lds + a.nstage * a.stage_bytes;
-        const int64_t tile = lds_list ? lds_list[pos - t0] : a.list[pos];
 #pragma unroll
         for (int k = 0; k < kMaxPW; ++k) {
             if (k < per_wave) {
@@ -1986,7 +1980,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
         for (int q = 0; q < NQ; ++q) kval[q] = q < nq;
 
         for (int k = 0; k < NS - 1; ++k)
-            if (t0 + k < t1) stage(k, t0 + k);
+            if (t0 + k < t1) stage(k, tile_at(t0 + k));
         int bcur = 0, bnext = NS - 1;  // stage of tile t, stage tile t+NS-1 goes to
         for (int64_t t = t0; t < t1; ++t) {
             // stages t+1 .. t+NS-2 may stay in flight
@@ -1995,7 +1989,7 @@ __global__ __launch_bounds__(kDwThreads, 1) void mlp_dw_kernel(DwArgs a) {
             wait_pieces(per_wave * static_cast<int>(ahead));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
-            if (t + NS - 1 < t1) stage(bnext, t + NS - 1);
+            if (t + NS - 1 < t1) stage(bnext, tile_at(t + NS - 1));
             bnext = bnext + 1 == NS ? 0 : bnext + 1;
             const char* buf = lds + bcur * a.stage_bytes;
             bcur = bcur + 1 == NS ? 0 : bcur + 1;
@@ -2569,7 +2563,8 @@ int launch_bwd_rbm(const MlpPlan& p, const BwdrArgs& a, hipStream_t s) {
         set_error("nr_mlp_backward_dx: %zu bytes of LDS exceed 160 KiB", lds);
         return NR_EARG;
     }
-    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, kRbmWaves))), block(kRbmWaves * 64);
+    // every part of every segment (mlp_bwd_rbm_kernel's workgroup mapping)
+    const dim3 grid(static_cast<unsigned>(a.nseg * (kSegTiles / kRbmWaves))), block(kRbmWaves * 64);
     hipLaunchKernelGGL((mlp_bwd_rbm_kernel<PREC>), grid, block, lds, s, a);
     return check_launch("nr_mlp_backward_dx");
 }
@@ -2592,7 +2587,8 @@ int launch_bwd(const MlpPlan& p, BwdArgs& a, hipStream_t s) {
         set_error("nr_mlp_backward_dx: %zu bytes of LDS exceed 160 KiB", lds);
         return NR_EARG;
     }
-    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, (NT / 64) * TPW))), block(NT);
+    // every part of every segment (mlp_bwd_kernel's workgroup mapping)
+    const dim3 grid(static_cast<unsigned>(a.nseg * (kSegTiles / (NT / 64)))), block(NT);
 #define NR_BWD(XB_, DB_)                                                                              \
     if (p.XB == XB_ && p.DB == DB_) {                                                                 \
         hipLaunchKernelGGL((mlp_bwd_kernel<PREC, XB_, DB_, TPW, G, NT, WX>), grid, block, lds, s, a); \
@@ -2960,7 +2956,7 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     const MlpSizes z = make_sizes(p, M);
     NR_REQUIRE(z.tiles_alloc < (int64_t{1} << 32), "nr_mlp_backward_dx: M beyond 2^37 samples");
     // the segment lists of the active tiles (every tile with cfg->dense_backward); the dX
-    // launch's first workgroup concatenates them into the dW kernel's list
+    // launch concatenates them into the dW kernel's list (place_segment)
     char* wsb = static_cast<char*>(workspace);
     uint8_t* tflags = reinterpret_cast<uint8_t*>(wsb + z.flags_off);
     uint32_t* seglist = reinterpret_cast<uint32_t*>(wsb + z.list_off + 0);
