@@ -24,6 +24,7 @@
 // rebuilds sample-major operands with the gfx950 transpose read
 // ds_read_b64_tr_b16 (bf16) or strided ds_read_b32 (fp32).
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <utility>
@@ -1189,23 +1190,63 @@ __global__ __launch_bounds__(NT, 1) void mlp_fwd_kernel(FwdArgs a) {
     }
 }
 
-// The dW kernel's work list: the segment lists of tile_flags_kernel concatenated in
-// segment order (every active tile once, in increasing order) and their total.  Each
-// segment's entries are placed by wave 0 of the dX workgroup that leads the segment (the
-// first of its kSegTiles / waves-per-workgroup workgroups), after its own tiles: it sums
-// the counts of the segments before it (independent loads, one wave reduction) and
-// copies the segment's entries with one coalesced load and store.
-__device__ __forceinline__ void place_segment(const uint32_t* __restrict__ seg_list,
-                                              const uint32_t* __restrict__ seg_count, int64_t nseg, int64_t sg,
-                                              uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
+// Active tiles of a segment from its flags (tile_flags_kernel), one wave: lane l holds
+// flag word l (tiles 4l .. 4l+3 of the segment, one byte each, 0 or 1), its count and the
+// wave's inclusive scan of the counts.
+struct SegFlags {
+    uint32_t word;
+    int count, incl, total;
+};
+__device__ __forceinline__ SegFlags seg_flags(const uint8_t* __restrict__ flags, int64_t sg) {
+    static_assert(kSegTiles == 4 * 64, "one flag word per lane");
+    const int lane = threadIdx.x & 63;
+    SegFlags f;
+    f.word = reinterpret_cast<const uint32_t*>(flags + sg * kSegTiles)[lane];
+    f.count = __popc(f.word);
+    f.incl = f.count;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(f.incl, d);
+        if (lane >= d) f.incl += o;
+    }
+    f.total = __builtin_amdgcn_readfirstlane(__shfl(f.incl, 63));
+    return f;
+}
+
+// The tile of the segment's k-th active tile (k < f.total; wave-uniform result).
+__device__ __forceinline__ int64_t seg_entry(const SegFlags& f, int64_t sg, int k) {
+    const uint64_t over = __ballot(f.incl > k);
+    const int L = __builtin_ctzll(over);  // the lane whose word holds entry k
+    const uint32_t w = __builtin_amdgcn_readfirstlane(__shfl(f.word, L));
+    int r = k - __builtin_amdgcn_readfirstlane(__shfl(f.incl - f.count, L));
+    int b = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const bool set = (w >> (8 * q)) & 1u;
+        if (set && r == 0) b = q;
+        r -= set ? 1 : 0;
+        if (r < 0) r = 1 << 20;  // found: no later byte matches
+    }
+    return sg * kSegTiles + 4 * L + b;
+}
+
+// The dW kernel's work list: every active tile once, in increasing order, and their
+// total.  Each segment's tiles are placed by wave 0 of the dX workgroup that leads the
+// segment (part 0), after its own tiles: the 64-tile block counts of the segments before
+// it (independent loads, one wave reduction) give its first slot, and each lane writes
+// the active tiles of its flag word.
+__device__ __forceinline__ void place_segment(const SegFlags& f, const uint32_t* __restrict__ blk_count, int64_t nseg,
+                                              int64_t sg, uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
     const int lane = threadIdx.x & 63;
     uint32_t before = 0;
-    for (int64_t q = lane; q < sg; q += 64) before += seg_count[q];
+    for (int64_t q = lane; q < sg * (kSegTiles / 64); q += 64) before += blk_count[q];
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) before += __shfl_xor(before, d);
-    const uint32_t c = seg_count[sg];
-    if (static_cast<uint32_t>(lane) < c) list[before + lane] = seg_list[sg * kSegTiles + lane];
-    if (sg == nseg - 1 && lane == 0) *count = before + c;
+    uint32_t slot = before + static_cast<uint32_t>(f.incl - f.count);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if ((f.word >> (8 * q)) & 1u) list[slot++] = static_cast<uint32_t>(sg * kSegTiles + 4 * lane + q);
+    if (sg == nseg - 1 && lane == 0) *count = before + static_cast<uint32_t>(f.total);
 }
 
 #include "mlp_fwd_rbm.inc"
@@ -1227,8 +1268,8 @@ struct BwdArgs {
     const char* saved;
     char* ws;
     int64_t M, tiles;
-    const uint32_t* list;       // segment lists of the active tiles (tile_flags_kernel)
-    const uint32_t* seg_count;
+    const uint8_t* flags;       // active tiles (tile_flags_kernel) and their 64-tile block counts
+    const uint32_t* blk_count;
     int64_t nseg;
     uint32_t* dw_list;          // the dW kernel's list and count (place_segment)
     uint32_t* count;
@@ -1255,22 +1296,22 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     static_assert(TPW == 1, "the active-tile list gives each wave one tile");
     const int64_t my_seg = blockIdx.x % a.nseg;
     const int part = static_cast<int>(blockIdx.x / a.nseg);
-    const int64_t first_slot = my_seg * kSegTiles + part * (NT / 64), slot = first_slot + wv;
-    // both scalar loads in flight together: past the segment's count the list holds kTileNone
-    const uint32_t first = a.list[first_slot], mine = a.list[slot];
-    const bool leader = part == 0 && wv == 0;  // wave 0 of a segment's first workgroup
-    if (first == kTileNone) {  // workgroup-uniform
-        if (leader) place_segment(a.list, a.seg_count, a.nseg, my_seg, a.dw_list, a.count);
+    const SegFlags sf = seg_flags(a.flags, my_seg);  // every wave: the same counts
+    const bool leader = part == 0 && wv == 0;          // wave 0 of a segment's first workgroup
+    if (part * (NT / 64) >= sf.total) {                // workgroup-uniform
+        if (leader) place_segment(sf, a.blk_count, a.nseg, my_seg, a.dw_list, a.count);
         return;
     }
-    const int64_t tile0 = mine != kTileNone ? static_cast<int64_t>(mine) : 0;
+    const int k = part * (NT / 64) + wv;
+    const bool live = k < sf.total;
+    const int64_t tile0 = live ? seg_entry(sf, my_seg, k) : 0;
     const int n = a.n_layers;
     const u32x4* masks = reinterpret_cast<const u32x4*>(a.saved + a.mask_off);
     bool tok[TPW];
     unsigned tokm = 0u;
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        tok[t] = mine != kTileNone;
+        tok[t] = live;
         tokm |= (tok[t] ? 1u : 0u) << t;
     }
     // each dz image is saved while the next stream consumes it
@@ -1501,7 +1542,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
             }
         }
     }
-    if (leader) place_segment(a.list, a.seg_count, a.nseg, my_seg, a.dw_list, a.count);
+    if (leader) place_segment(sf, a.blk_count, a.nseg, my_seg, a.dw_list, a.count);
 }
 
 // ------------------------------------------------ input gradients ------
@@ -1672,25 +1713,22 @@ __global__ __launch_bounds__(kDinNT) void mlp_dinput_kernel(DinArgs a) {
 // tile of such samples only adds exact zeros to dW, so the dX chain, the dW GEMM and
 // the input gradients run over the tiles with ANY nonzero incoming gradient (computed
 // from the values, never assumed).  One launch, no global scan: the tiles form
-// segments of kSegTiles; workgroup s writes segment s's flags, its active tiles in
-// tile order at seg_list[s * kSegTiles ...] (kTileNone past them) and their count.  The
-// dX kernels take a segment's entries eight (four) at a time and concatenate the
-// segments into the dW kernel's list (place_segment), which that kernel splits evenly over
-// its chunks.  With every tile active, each kernel sees exactly the dense form's tiles in
-// order.
-constexpr int kTileFlagThreads = 256;  // 4 waves x 16 tiles per workgroup = one segment
-static_assert(kSegTiles == 4 * 16, "one tile_flags_kernel workgroup per segment");
+// segments of kSegTiles; the launch writes one flag byte per tile and the active count
+// of every 64-tile block.  A dX workgroup takes eight (four) of its segment's active
+// tiles, found from the segment's 256 flag bytes (one word per lane, a wave scan), and
+// the segments' leaders concatenate them into the dW kernel's list (place_segment), which
+// that kernel splits evenly over its chunks.  With every tile active, each kernel sees
+// exactly the dense form's tiles in order.
+constexpr int kTileFlagThreads = 256;  // 4 waves x 16 tiles: one 64-tile block per workgroup
 
 __global__ __launch_bounds__(kTileFlagThreads) void tile_flags_kernel(const float* __restrict__ g_rgb,
                                                                       const float* __restrict__ g_sigma, int64_t M,
                                                                       int64_t tiles, int dense,
                                                                       uint8_t* __restrict__ flags,
-                                                                      uint32_t* __restrict__ seg_list,
-                                                                      uint32_t* __restrict__ seg_count) {
-    __shared__ uint32_t wcnt[4];
+                                                                      uint32_t* __restrict__ blk_count) {
+    __shared__ uint32_t wcnt[kTileFlagThreads / 64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t seg0 = static_cast<int64_t>(blockIdx.x) * kSegTiles;
-    const int64_t tw = seg0 + wv * 16;
+    const int64_t tw = static_cast<int64_t>(blockIdx.x) * 64 + wv * 16;
     bool nz[8];
     // lanes 0-31: tile tw + 2 it, lanes 32-63: tile tw + 2 it + 1 (one sample each)
 #pragma unroll
@@ -1707,26 +1745,17 @@ __global__ __launch_bounds__(kTileFlagThreads) void tile_flags_kernel(const floa
         }
         nz[it] = v;
     }
-    uint32_t mask = 0;  // bit k: tile tw + k is active (wave-uniform)
+    uint32_t mask = 0;  // bit k: tile tw + k is active (wave-uniform); tiles past `tiles`: 0
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
         const uint64_t b = __ballot(nz[it]);
         mask |= (static_cast<uint32_t>(b & 0xffffffffull) != 0 ? 1u : 0u) << (2 * it);
         mask |= (static_cast<uint32_t>(b >> 32) != 0 ? 1u : 0u) << (2 * it + 1);
     }
-    if (lane < 16 && tw + lane < tiles) flags[tw + lane] = static_cast<uint8_t>((mask >> lane) & 1u);
+    if (lane < 16) flags[tw + lane] = static_cast<uint8_t>((mask >> lane) & 1u);
     if (lane == 0) wcnt[wv] = __popc(mask);
     __syncthreads();
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        before += q < wv ? wcnt[q] : 0u;
-        total += wcnt[q];
-    }
-    if (lane < 16 && ((mask >> lane) & 1u))
-        seg_list[seg0 + before + __popc(mask & ((1u << lane) - 1u))] = static_cast<uint32_t>(tw + lane);
-    if (threadIdx.x < kSegTiles && threadIdx.x >= total) seg_list[seg0 + threadIdx.x] = kTileNone;
-    if (threadIdx.x == 0) seg_count[blockIdx.x] = total;
+    if (threadIdx.x == 0) blk_count[blockIdx.x] = ((wcnt[0] + wcnt[1]) + wcnt[2]) + wcnt[3];
 }
 
 // ------------------------------------------------------------------ dW ----
@@ -2535,15 +2564,34 @@ int launch_fwd(const MlpPlan& p, FwdArgs& a, hipStream_t s) {
     return NR_EARG;
 }
 
+// waves per workgroup of the row-block-major forward for a launch of `tiles` tiles: 8,
+// or 4 when eight-wave workgroups would leave half the 256 CUs idle (a graph-replayed
+// 512-ray step's coarse net: 1024 tiles; 0.068 -> 0.055 ms).  At 3072 tiles (the fine
+// net of that step) four waves lose (0.166 -> 0.176 ms) and the dX chain keeps eight:
+// the coarse backward overlaps the fine forward there and should not take every CU
+// (profiles/r06_rbm_waves.txt).  NR_RBM_WAVES=4|8 forces one (A/B measurements).
+inline int rbm_waves(int64_t tiles) {
+    static const int forced = [] {
+        const char* e = std::getenv("NR_RBM_WAVES");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (forced == 4 || forced == 8) return forced;
+    return ceil_div_ll(tiles, 8) <= 128 ? 4 : 8;
+}
+
 template <int PREC, bool TRAIN>
 int launch_fwd_rbm(const MlpPlan& p, const RbmArgs& a, hipStream_t s) {
     // every chunk fits a slot (checked at compile time per layer shape)
-    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, kRbmWaves))), block(kRbmWaves * 64);
-    const size_t lds = rbm_lds_bytes(p.XB);
-#define NR_FWDR(XB_, DB_)                                                                            \
-    if (p.XB == XB_ && p.DB == DB_) {                                                                \
-        hipLaunchKernelGGL((mlp_fwd_rbm_kernel<PREC, XB_, DB_, TRAIN>), grid, block, lds, s, a);      \
-        return check_launch("nr_mlp_forward");                                                       \
+    const int w = rbm_waves(a.tiles);
+    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, w))), block(w * 64);
+    const size_t lds = rbm_lds_bytes(p.XB, w);
+#define NR_FWDR(XB_, DB_)                                                                               \
+    if (p.XB == XB_ && p.DB == DB_) {                                                                   \
+        if (w == 4)                                                                                     \
+            hipLaunchKernelGGL((mlp_fwd_rbm_kernel<PREC, XB_, DB_, TRAIN, 4>), grid, block, lds, s, a); \
+        else                                                                                            \
+            hipLaunchKernelGGL((mlp_fwd_rbm_kernel<PREC, XB_, DB_, TRAIN, 8>), grid, block, lds, s, a); \
+        return check_launch("nr_mlp_forward");                                                          \
     }
     NR_FWDR(2, 1)
 #ifndef NR_MLP_DEV
@@ -2558,14 +2606,15 @@ int launch_fwd_rbm(const MlpPlan& p, const RbmArgs& a, hipStream_t s) {
 
 template <int PREC>
 int launch_bwd_rbm(const MlpPlan& p, const BwdrArgs& a, hipStream_t s) {
-    const size_t lds = bwdr_lds_bytes(p.n_mask);
+    constexpr int W = kRbmWaves;
+    const size_t lds = bwdr_lds_bytes(p.n_mask, W);
     if (lds > 160 * 1024) {
         set_error("nr_mlp_backward_dx: %zu bytes of LDS exceed 160 KiB", lds);
         return NR_EARG;
     }
     // every part of every segment (mlp_bwd_rbm_kernel's workgroup mapping)
-    const dim3 grid(static_cast<unsigned>(a.nseg * (kSegTiles / kRbmWaves))), block(kRbmWaves * 64);
-    hipLaunchKernelGGL((mlp_bwd_rbm_kernel<PREC>), grid, block, lds, s, a);
+    const dim3 grid(static_cast<unsigned>(a.nseg * (kSegTiles / W))), block(W * 64);
+    hipLaunchKernelGGL((mlp_bwd_rbm_kernel<PREC, W>), grid, block, lds, s, a);
     return check_launch("nr_mlp_backward_dx");
 }
 
@@ -2955,16 +3004,15 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const MlpSizes z = make_sizes(p, M);
     NR_REQUIRE(z.tiles_alloc < (int64_t{1} << 32), "nr_mlp_backward_dx: M beyond 2^37 samples");
-    // the segment lists of the active tiles (every tile with cfg->dense_backward); the dX
-    // launch concatenates them into the dW kernel's list (place_segment)
+    // the active tiles' flags (every tile with cfg->dense_backward); the dX launch
+    // concatenates each segment's into the dW kernel's list (place_segment)
     char* wsb = static_cast<char*>(workspace);
     uint8_t* tflags = reinterpret_cast<uint8_t*>(wsb + z.flags_off);
-    uint32_t* seglist = reinterpret_cast<uint32_t*>(wsb + z.list_off + 0);
-    uint32_t* segcnt = reinterpret_cast<uint32_t*>(wsb + z.segcnt_off);
+    uint32_t* blkcnt = reinterpret_cast<uint32_t*>(wsb + z.blkcnt_off);
     uint32_t* dwlist = reinterpret_cast<uint32_t*>(wsb + z.dwlist_off);
     uint32_t* tcount = reinterpret_cast<uint32_t*>(wsb + z.count_off);
-    hipLaunchKernelGGL(tile_flags_kernel, dim3(static_cast<unsigned>(z.nseg)), dim3(kTileFlagThreads), 0, s, g_rgb,
-                       g_sigma, M, z.tiles, p.dense_bwd, tflags, seglist, segcnt);
+    hipLaunchKernelGGL(tile_flags_kernel, dim3(static_cast<unsigned>(z.nseg * (kSegTiles / 64))),
+                       dim3(kTileFlagThreads), 0, s, g_rgb, g_sigma, M, z.tiles, p.dense_bwd, tflags, blkcnt);
     NR_LAUNCH_CHECK("nr_mlp_backward_dx (tile flags)");
     BwdArgs b;
     std::memset(&b, 0, sizeof(b));
@@ -2984,8 +3032,8 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     b.ws = static_cast<char*>(workspace);
     b.M = M;
     b.tiles = z.tiles;
-    b.list = seglist;
-    b.seg_count = segcnt;
+    b.flags = tflags;
+    b.blk_count = blkcnt;
     b.nseg = z.nseg;
     b.dw_list = dwlist;
     b.count = tcount;
@@ -3033,8 +3081,8 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
         r.ws = b.ws;
         r.M = M;
         r.tiles = z.tiles;
-        r.list = seglist;
-        r.seg_count = segcnt;
+        r.flags = tflags;
+        r.blk_count = blkcnt;
         r.nseg = z.nseg;
         r.dw_list = dwlist;
         r.count = tcount;

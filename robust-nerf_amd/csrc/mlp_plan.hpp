@@ -26,8 +26,7 @@ constexpr int kHB = kHidden / 32;      // hidden feature blocks
 constexpr int kMaxTrunk = 16;          // num_hidden_layers upper bound
 constexpr int kMaxMfmaLayers = kMaxTrunk + 2;  // trunk + feature + dir
 constexpr int kFragBytes = 1024;       // one wave-wide 16-B-per-lane operand fragment
-constexpr uint32_t kTileNone = 0xffffffffu;  // active-tile list slots past its count
-constexpr int kSegTiles = 64;  // tiles per segment of the active-tile list
+constexpr int kSegTiles = 256;  // tiles per segment of the active-tile list
 constexpr int kMaxJobs = kMaxTrunk + 8;  // dW jobs: x-jobs + trunk h-jobs + feat + heads + dir
 constexpr int kMaxSeg = 2;
 constexpr int kMaxJobSeg = 4;            // tensors on either side of a dW job
@@ -149,9 +148,8 @@ struct MlpSizes {
     int max_chunks;                    // per-chunk slab sets allocated (the largest job_chunks)
     int64_t slab_off;                  // bytes
     int64_t nseg;                      // segments of kSegTiles tiles
-    // bytes: tile flags (u8); segment lists (kSegTiles u32 each, kTileNone-padded) and counts;
-    // the dW kernel's concatenated list and its total (u32)
-    int64_t flags_off, list_off, segcnt_off, dwlist_off, count_off;
+    // bytes: tile flags (u8, nseg * kSegTiles); 64-tile block counts; the dW list; its length
+    int64_t flags_off, blkcnt_off, dwlist_off, count_off;
     int64_t ws_bytes;
 };
 
