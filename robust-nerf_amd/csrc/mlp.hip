@@ -2445,16 +2445,29 @@ __device__ __forceinline__ void put_image(char* packed, uint32_t e, float p) {
 
 __global__ void __launch_bounds__(kSumsqThreads) adam_multi_kernel(AdamMultiArgs a) {
     const AdamSpanDev& s = a.s[blockIdx.y];
-    const float coef = s.partials ? clip_coef(block_sum_fixed(s.partials[threadIdx.x]), s.max_norm) : 1.0f;
     const float step_size = a.sched ? a.sched[0] : a.step_size, bc2_sqrt = a.sched ? a.sched[1] : a.bc2_sqrt;
     const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
     const int64_t t0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const int64_t n = s.n;
     // 16-B accesses when every buffer (and the table's slot rows) allows them
     const int64_t n4 = (n % 4 == 0) ? n / 4 : 0;
+    float4 P, G, M, V;
+    u32x4 E[kPackSlots];
+    auto load = [&](int64_t i) {
+        P = reinterpret_cast<const float4*>(s.p)[i];
+        G = reinterpret_cast<const float4*>(s.g)[i];
+        M = reinterpret_cast<const float4*>(s.m)[i];
+        V = reinterpret_cast<const float4*>(s.v)[i];
+        if (s.table)
+#pragma unroll
+            for (int sl = 0; sl < kPackSlots; ++sl) E[sl] = reinterpret_cast<const u32x4*>(s.table + sl * n)[i];
+    };
+    // the first element's loads go out before the clip coefficient's 256 partials are
+    // summed (per wave, no barrier: the grid is one element per thread at NeRF sizes)
+    if (t0 < n4) load(t0);
+    const float coef = s.partials ? clip_coef(wave_sum_fixed(s.partials), s.max_norm) : 1.0f;
     for (int64_t i = t0; i < n4; i += stride) {
-        float4 P = reinterpret_cast<float4*>(s.p)[i], G = reinterpret_cast<float4*>(s.g)[i];
-        float4 M = reinterpret_cast<float4*>(s.m)[i], V = reinterpret_cast<float4*>(s.v)[i];
+        if (i != t0) load(i);
         adam_one(P.x, G.x, M.x, V.x, coef, a.omb1, a.b2, a.omb2, step_size, bc2_sqrt, a.eps);
         adam_one(P.y, G.y, M.y, V.y, coef, a.omb1, a.b2, a.omb2, step_size, bc2_sqrt, a.eps);
         adam_one(P.z, G.z, M.z, V.z, coef, a.omb1, a.b2, a.omb2, step_size, bc2_sqrt, a.eps);
@@ -2466,24 +2479,23 @@ __global__ void __launch_bounds__(kSumsqThreads) adam_multi_kernel(AdamMultiArgs
         if (s.table) {
 #pragma unroll
             for (int sl = 0; sl < kPackSlots; ++sl) {
-                const u32x4 e = reinterpret_cast<const u32x4*>(s.table + sl * n)[i];
-                put_image(s.packed, e.x, P.x);
-                put_image(s.packed, e.y, P.y);
-                put_image(s.packed, e.z, P.z);
-                put_image(s.packed, e.w, P.w);
+                put_image(s.packed, E[sl].x, P.x);
+                put_image(s.packed, E[sl].y, P.y);
+                put_image(s.packed, E[sl].z, P.z);
+                put_image(s.packed, E[sl].w, P.w);
             }
         }
     }
     for (int64_t i = 4 * n4 + t0; i < n; i += stride) {
-        float P = s.p[i], G = s.g[i], M = s.m[i], V = s.v[i];
-        adam_one(P, G, M, V, coef, a.omb1, a.b2, a.omb2, step_size, bc2_sqrt, a.eps);
-        s.p[i] = P;
-        s.g[i] = G;
-        s.m[i] = M;
-        s.v[i] = V;
+        float P1 = s.p[i], G1 = s.g[i], M1 = s.m[i], V1 = s.v[i];
+        adam_one(P1, G1, M1, V1, coef, a.omb1, a.b2, a.omb2, step_size, bc2_sqrt, a.eps);
+        s.p[i] = P1;
+        s.g[i] = G1;
+        s.m[i] = M1;
+        s.v[i] = V1;
         if (s.table)
 #pragma unroll
-            for (int sl = 0; sl < kPackSlots; ++sl) put_image(s.packed, s.table[sl * n + i], P);
+            for (int sl = 0; sl < kPackSlots; ++sl) put_image(s.packed, s.table[sl * n + i], P1);
     }
 }
 

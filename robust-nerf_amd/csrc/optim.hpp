@@ -23,6 +23,22 @@ __device__ __forceinline__ float block_sum_fixed(float s) {
     return t;
 }
 
+// block_sum_fixed over kSumsqThreads values x[0..), computed by ONE wave without LDS or a
+// barrier: lane l folds x[64 w + l] through the same xor tree per w, then the four wave
+// sums in the same order -- the identical float result in every wave of every block
+__device__ __forceinline__ float wave_sum_fixed(const float* __restrict__ x) {
+    static_assert(kSumsqThreads == 256, "four waves' worth of values");
+    const int l = threadIdx.x & 63;
+    float r[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) r[w] = x[64 * w + l];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) r[w] += __shfl_xor(r[w], off);
+    return ((r[0] + r[1]) + r[2]) + r[3];
+}
+
 // clip_grad_norm_ coefficient from a squared norm (train.py:115)
 __device__ __forceinline__ float clip_coef(float sumsq, float max_norm) {
     const float c = max_norm / (sqrtf(sumsq) + 1e-6f);

@@ -256,12 +256,20 @@ class Trainer:
                           coarse_backward=coarse_backward if cs is not None else None,
                           target_rgb=target_rgb, loss_scale=gs)
         if cs is not None:
+            main = torch.cuda.current_stream(rays_o.device)
             loss_f = out["loss_fine"]
-            loss_f.backward(ops.unit_grad(rays_o.device))
-            torch.cuda.current_stream(rays_o.device).wait_stream(cs)  # join the coarse chain
             loss_c = early["loss_c"].detach()
-            loss = loss_c + loss_f.detach()  # the backward already ran: the value only
-            metrics = {"loss_coarse": loss_c.detach(), "loss_fine": loss_f.detach()}
+            # the summed value on the coarse stream, beside the fine backward (the backward
+            # already ran for loss_c; d(loss_c + loss_f) = d loss_f for the fine net)
+            cs.wait_stream(main)
+            lf = loss_f.detach()
+            lf.record_stream(cs)
+            with torch.cuda.stream(cs):
+                loss = loss_c + lf
+            loss.record_stream(main)
+            loss_f.backward(ops.unit_grad(rays_o.device))
+            main.wait_stream(cs)  # join the coarse chain
+            metrics = {"loss_coarse": loss_c, "loss_fine": lf}
         else:
             loss_c = out["loss_coarse"]
             loss = loss_c
@@ -291,8 +299,9 @@ class GraphedTrainer:
     step) exceeds it -- small per-GPU batches such as BASELINE cfg #4's 512 rays per rank.
 
     Everything the replay needs is on the device: the rays go through static input
-    buffers, torch's graph-safe RNG draws the jitter / inverse-CDF uniforms (or the
-    caller passes them as static inputs), the fused Adam launch rewrites the packed
+    buffers, the jitter / inverse-CDF uniforms are drawn by torch.rand into static
+    buffers before each replay (or the caller passes them; torch's graph-safe RNG inside
+    the graph when the step also draws noise), the fused Adam launch rewrites the packed
     images, and the two step-dependent Adam scalars come from an 8-byte device pair
     written before each replay (``FusedAdam.device_sched``); the LR schedule and the
     optimizer's step counters advance on the host exactly as in ``Trainer.step``.
@@ -313,6 +322,21 @@ class GraphedTrainer:
         self.static = [t.detach().clone() for t in (rays_o, rays_d, target_rgb)]
         self.static_rand = [None if t is None else t.detach().clone() for t in (t_rand, u)]
         dev = rays_o.device
+        # randoms the caller does not inject are drawn into static buffers right before
+        # each step (eager warm-ups and every replay) rather than inside the graph: the
+        # same torch.rand calls in the same order as the eager step makes them, so the
+        # numbers are the eager step's, and a replay skips torch's graph-RNG prologue
+        # (two fill launches before every replay of a graph that draws).  Only when the
+        # step draws nothing else (raw_noise_std == 0), which would interleave with them
+        rc = trainer.render_config
+        self._predraw = []
+        if t_rand is None and u is None and rc.perturb and not rc.raw_noise_std:
+            B = rays_o.shape[0]
+            self.static_rand[0] = torch.empty(B, rc.num_samples, device=dev)
+            self._predraw.append(self.static_rand[0])
+            if rc.use_hierarchical and trainer.model_fine is not None:
+                self.static_rand[1] = torch.empty(B, rc.num_samples_fine, device=dev)
+                self._predraw.append(self.static_rand[1])
         self.sched = torch.zeros(2, device=dev, dtype=torch.float32)
         # pinned staging ring for the per-step pair: a slot is rewritten only after the
         # copy that read it has run (its event), however far the host runs ahead
@@ -329,6 +353,7 @@ class GraphedTrainer:
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for _ in range(warmup):
+                self._draw()
                 trainer.step(*self.static, *self.static_rand)
         torch.cuda.current_stream(dev).wait_stream(side)
         # capture one step; its host-side bookkeeping (Adam step counters, LR scheduler)
@@ -350,6 +375,10 @@ class GraphedTrainer:
         # another shape, see train.train) use the host scalars again
         opt.device_sched = None
         self._bound = self._bound_buffers()
+
+    def _draw(self) -> None:
+        for t in self._predraw:
+            t.uniform_()  # torch.rand(shape) of the eager step, into the static buffer
 
     def _bound_buffers(self):
         """The device tensors whose addresses the captured graph holds (strong references)."""
@@ -390,6 +419,8 @@ class GraphedTrainer:
         """Replay one training step on these rays (copied into the static buffers; None:
         the buffers as they are).  Returns the captured metrics (device tensors that every
         replay overwrites).  Eager ``trainer.step`` calls may be interleaved (same state)."""
+        if self._predraw and (t_rand is None) != (u is None) and len(self._predraw) == 2:
+            raise ValueError("GraphedTrainer: inject both t_rand and u, or neither")
         dsts, srcs = [], []
         for dst, src in zip(self.static + self.static_rand, (rays_o, rays_d, target_rgb, t_rand, u)):
             if src is not None:
@@ -403,6 +434,8 @@ class GraphedTrainer:
         else:
             for d, x in zip(dsts, srcs):
                 d.copy_(x)
+        if self._predraw and t_rand is None:
+            self._draw()
         self._check_bound()
         opt = self.trainer.optimizer
         group = opt.param_groups[0]

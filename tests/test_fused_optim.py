@@ -187,3 +187,35 @@ def test_graphed_trainer_equals_eager_trainer(precision):
     assert eager.optimizer.param_groups[0]["lr"] == tr_g.optimizer.param_groups[0]["lr"]
     pe, pg = eager.params[0], tr_g.params[0]
     assert int(eager.optimizer.state[pe]["step"]) == int(tr_g.optimizer.state[pg]["step"]) == 7
+
+
+def test_graphed_trainer_draws_the_eager_randoms():
+    """Without injected randoms, GraphedTrainer draws the jitter and inverse-CDF uniforms
+    with torch.rand into its static buffers before each replay (no RNG inside the graph):
+    the same draws, in the same order, as the eager Trainer's own torch.rand calls, so
+    from the same seed both train bit-identically (coarse stream on: 512 rays)."""
+    from noisy_src.config import ModelConfig, RenderConfig
+    from noisy_src.engine import GraphedTrainer, Trainer
+    from noisy_src.model import create_nerf
+    rc = RenderConfig(num_samples=32, num_samples_fine=64)
+    trainers = []
+    for _ in range(2):
+        torch.manual_seed(5)
+        mc, mf = create_nerf(ModelConfig(precision="bf16"))
+        trainers.append(Trainer(mc.to(DEV), mf.to(DEV), rc, coarse_stream="auto"))
+    eager, tr_g = trainers
+    g = torch.Generator().manual_seed(29)
+    B = 512
+    o = (torch.randn(B, 3, generator=g) * 0.1 + torch.tensor([0.0, 0.0, 4.0])).to(DEV)
+    dd = torch.nn.functional.normalize(torch.randn(B, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, -1.0]),
+                                       dim=-1).to(DEV)
+    tgt = torch.rand(B, 3, generator=g).to(DEV)
+    torch.manual_seed(77)
+    le = [float(eager.step(o, dd, tgt)["loss"]) for _ in range(6)]
+    torch.manual_seed(77)
+    graphed = GraphedTrainer(tr_g, o, dd, tgt, warmup=2)
+    assert tr_g.last_step_coarse_stream
+    lg = [float(graphed.step()["loss"]) for _ in range(4)]  # steps 3-6 (the warm-ups were 1-2)
+    assert le[2:] == lg, (le, lg)
+    for na, nb in ((eager.model_coarse, tr_g.model_coarse), (eager.model_fine, tr_g.model_fine)):
+        assert torch.equal(na.flat_params(), nb.flat_params())
