@@ -1197,11 +1197,14 @@ struct SegFlags {
     uint32_t word;
     int count, incl, total;
 };
-__device__ __forceinline__ SegFlags seg_flags(const uint8_t* __restrict__ flags, int64_t sg) {
+__device__ __forceinline__ uint32_t seg_flag_word(const uint8_t* __restrict__ flags, int64_t sg) {
     static_assert(kSegTiles == 4 * 64, "one flag word per lane");
+    return reinterpret_cast<const uint32_t*>(flags + sg * kSegTiles)[threadIdx.x & 63];
+}
+__device__ __forceinline__ SegFlags seg_scan(uint32_t word) {
     const int lane = threadIdx.x & 63;
     SegFlags f;
-    f.word = reinterpret_cast<const uint32_t*>(flags + sg * kSegTiles)[lane];
+    f.word = word;
     f.count = __popc(f.word);
     f.incl = f.count;
 #pragma unroll
@@ -1232,21 +1235,99 @@ __device__ __forceinline__ int64_t seg_entry(const SegFlags& f, int64_t sg, int 
 
 // The dW kernel's work list: every active tile once, in increasing order, and their
 // total.  Each segment's tiles are placed by wave 0 of the dX workgroup that leads the
-// segment (part 0), after its own tiles: the 64-tile block counts of the segments before
-// it (independent loads, one wave reduction) give its first slot, and each lane writes
-// the active tiles of its flag word.
-__device__ __forceinline__ void place_segment(const SegFlags& f, const uint32_t* __restrict__ blk_count, int64_t nseg,
-                                              int64_t sg, uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
+// segment (part 0), after its own tiles, from `before` (the active tiles of the segments
+// before it, select_tile): each lane writes the active tiles of its flag word.
+__device__ __forceinline__ void place_segment(const SegFlags& f, uint32_t before, int64_t nseg, int64_t sg,
+                                              uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
     const int lane = threadIdx.x & 63;
-    uint32_t before = 0;
-    for (int64_t q = lane; q < sg * (kSegTiles / 64); q += 64) before += blk_count[q];
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) before += __shfl_xor(before, d);
     uint32_t slot = before + static_cast<uint32_t>(f.incl - f.count);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
         if ((f.word >> (8 * q)) & 1u) list[slot++] = static_cast<uint32_t>(sg * kSegTiles + 4 * lane + q);
     if (sg == nseg - 1 && lane == 0) *count = before + static_cast<uint32_t>(f.total);
+}
+
+// A dX wave's tile.  Every workgroup reads the 64-tile block counts of the whole launch
+// (tile_flags_kernel; one uint4 per segment, from L2) and its segment's flags, in one
+// round of loads:
+//  * every tile active (the dense case: bare-init training, cfg->dense_backward):
+//    workgroup b runs tiles W b .. W b + W - 1, the layout's own order (no lists; dW
+//    takes its identity path on count == tiles);
+//  * otherwise, segment-minor: workgroup b takes part j = b / nseg of segment b % nseg,
+//    i.e. the active tiles W j .. W j + W - 1 of that segment, so the workgroups with
+//    active tiles are dispatched first and spread over every XCD (blocks are dealt to
+//    XCDs round-robin); parts past a segment's count have nothing to do.
+// Measured (fine bf16 M=786432 dX, profiles/r06_tile_map_ab.txt): segment-minor in the
+// dense case costs ~7 % at M=786432 and ~20 % at 262144 (locality), segment-major in
+// the skipping case 1.67x at 37 % active.
+struct TileSel {
+    SegFlags sf;
+    int64_t seg, tile;
+    uint32_t before;   // skipping form: active tiles of the segments before seg
+    bool dense, live, idle, leader;
+};
+__device__ __forceinline__ TileSel select_tile(const uint8_t* __restrict__ flags,
+                                               const uint32_t* __restrict__ blk_count, int64_t nseg,
+                                               int64_t tiles, int W, int wv) {
+    constexpr int BPS = kSegTiles / 64;  // 64-tile blocks per segment
+    const int lane = threadIdx.x & 63;
+    const int64_t b = blockIdx.x;
+    TileSel t;
+    t.seg = b % nseg;
+    const int part = static_cast<int>(b / nseg);
+    // every load first (one round trip): the segment's flag word and the block counts,
+    // one uint4 (a segment's four blocks) per lane and 64 segments
+    static_assert(BPS == 4, "a segment's block counts are one uint4");
+    const uint32_t word = seg_flag_word(flags, t.seg);
+    const uint4* __restrict__ bc4 = reinterpret_cast<const uint4*>(blk_count);
+    uint32_t all = 0, before = 0;
+    for (int64_t s0 = 0; s0 < nseg; s0 += 4 * 64) {
+        uint4 c[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t sg = s0 + i * 64 + lane;
+            c[i] = sg < nseg ? bc4[sg] : uint4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t n = ((c[i].x + c[i].y) + c[i].z) + c[i].w;
+            all += n;
+            before += (s0 + i * 64 + lane) < t.seg ? n : 0u;
+        }
+    }
+    t.sf = seg_scan(word);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        all += __shfl_xor(all, d);
+        before += __shfl_xor(before, d);
+    }
+    t.before = __builtin_amdgcn_readfirstlane(before);
+    t.dense = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(all)) == tiles;
+    if (t.dense) {
+        const int64_t first = b * W;
+        t.tile = first + wv;
+        t.live = t.tile < tiles;
+        t.idle = first >= tiles;
+        t.leader = b == 0 && wv == 0;
+    } else {
+        const int k = part * W + wv;
+        t.idle = part * W >= t.sf.total;
+        t.live = k < t.sf.total;
+        t.tile = t.live ? seg_entry(t.sf, t.seg, k) : 0;
+        t.leader = part == 0 && wv == 0;
+    }
+    return t;
+}
+
+// the leader's share of the dW list (skipping form) or the dense count
+__device__ __forceinline__ void finish_tiles(const TileSel& t, int64_t nseg, int64_t tiles, uint32_t* __restrict__ list,
+                                             uint32_t* __restrict__ count) {
+    if (!t.leader) return;
+    if (t.dense) {
+        if ((threadIdx.x & 63) == 0) *count = static_cast<uint32_t>(tiles);
+    } else {
+        place_segment(t.sf, t.before, nseg, t.seg, list, count);
+    }
 }
 
 #include "mlp_fwd_rbm.inc"
@@ -1289,22 +1370,16 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ml = lane & 31;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // workgroup -> (segment, part j): segment-minor, so the active parts (small j) are
-    // the first workgroups dispatched and spread over every XCD; wave -> entry
-    // j * (NT / 64) + wv of the segment's list (one tile per wave); waves past its count
-    // run on zero inputs and store nothing
-    static_assert(TPW == 1, "the active-tile list gives each wave one tile");
-    const int64_t my_seg = blockIdx.x % a.nseg;
-    const int part = static_cast<int>(blockIdx.x / a.nseg);
-    const SegFlags sf = seg_flags(a.flags, my_seg);  // every wave: the same counts
-    const bool leader = part == 0 && wv == 0;          // wave 0 of a segment's first workgroup
-    if (part * (NT / 64) >= sf.total) {                // workgroup-uniform
-        if (leader) place_segment(sf, a.blk_count, a.nseg, my_seg, a.dw_list, a.count);
+    // wave -> its tile (select_tile; one tile per wave); waves without one run on zero
+    // inputs and store nothing
+    static_assert(TPW == 1, "the active-tile selection gives each wave one tile");
+    const TileSel ts = select_tile(a.flags, a.blk_count, a.nseg, a.tiles, NT / 64, wv);
+    if (ts.idle) {  // workgroup-uniform
+        finish_tiles(ts, a.nseg, a.tiles, a.dw_list, a.count);
         return;
     }
-    const int k = part * (NT / 64) + wv;
-    const bool live = k < sf.total;
-    const int64_t tile0 = live ? seg_entry(sf, my_seg, k) : 0;
+    const bool live = ts.live;
+    const int64_t tile0 = live ? ts.tile : 0;
     const int n = a.n_layers;
     const u32x4* masks = reinterpret_cast<const u32x4*>(a.saved + a.mask_off);
     bool tok[TPW];
@@ -1542,7 +1617,7 @@ __global__ __launch_bounds__(NT, 1) void mlp_bwd_kernel(BwdArgs a) {
             }
         }
     }
-    if (leader) place_segment(sf, a.blk_count, a.nseg, my_seg, a.dw_list, a.count);
+    finish_tiles(ts, a.nseg, a.tiles, a.dw_list, a.count);
 }
 
 // ------------------------------------------------ input gradients ------
@@ -1714,11 +1789,12 @@ __global__ __launch_bounds__(kDinNT) void mlp_dinput_kernel(DinArgs a) {
 // the input gradients run over the tiles with ANY nonzero incoming gradient (computed
 // from the values, never assumed).  One launch, no global scan: the tiles form
 // segments of kSegTiles; the launch writes one flag byte per tile and the active count
-// of every 64-tile block.  A dX workgroup takes eight (four) of its segment's active
-// tiles, found from the segment's 256 flag bytes (one word per lane, a wave scan), and
-// the segments' leaders concatenate them into the dW kernel's list (place_segment), which
-// that kernel splits evenly over its chunks.  With every tile active, each kernel sees
-// exactly the dense form's tiles in order.
+// of every 64-tile block.  The dX workgroups pick their tiles from those (select_tile:
+// the dense order when every tile is active, else eight (four) of a segment's active
+// tiles found by a wave scan of its 256 flag bytes), and the segments' leaders
+// concatenate them into the dW kernel's list (place_segment), which that kernel splits
+// evenly over its chunks.  With every tile active, each kernel sees exactly the dense
+// form's tiles in order.
 constexpr int kTileFlagThreads = 256;  // 4 waves x 16 tiles: one 64-tile block per workgroup
 
 __global__ __launch_bounds__(kTileFlagThreads) void tile_flags_kernel(const float* __restrict__ g_rgb,
@@ -3098,7 +3174,7 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
         r.nseg = z.nseg;
         r.dw_list = dwlist;
         r.count = tcount;
-        r.scratch_tile = z.tiles_alloc - 1;
+        r.scratch_base = z.tiles_alloc - kScratchTiles;
         r.n_layers = n;
         r.base = p.lin[n + 1].pk_bwdr;
         r.vrgb = p.vrgb;

@@ -26,6 +26,7 @@ constexpr int kHB = kHidden / 32;      // hidden feature blocks
 constexpr int kMaxTrunk = 16;          // num_hidden_layers upper bound
 constexpr int kMaxMfmaLayers = kMaxTrunk + 2;  // trunk + feature + dir
 constexpr int kFragBytes = 1024;       // one wave-wide 16-B-per-lane operand fragment
+constexpr int kScratchTiles = 64;  // dX waves without an active tile spread their stores over these
 constexpr int kSegTiles = 256;  // tiles per segment of the active-tile list
 constexpr int kMaxJobs = kMaxTrunk + 8;  // dW jobs: x-jobs + trunk h-jobs + feat + heads + dir
 constexpr int kMaxSeg = 2;
@@ -138,7 +139,8 @@ bool make_plan(const NrMlpConfig* cfg, MlpPlan* p, const char** why);
 // Byte sizes / offsets that depend on the number of samples.
 struct MlpSizes {
     int64_t tiles;
-    int64_t tiles_alloc;  // tiles rounded up to whole 16-tile groups: every fwd/bwd wave may store its tile
+    int64_t tiles_alloc;  // tiles rounded up to whole 16-tile groups (every fwd wave may store its tile),
+                          // then kScratchTiles scratch tiles (dX waves without a tile store there)
     int64_t saved_off[kMaxTrunk + 4];  // bytes
     int64_t mask_off;                  // bytes
     int64_t saved_bytes;
