@@ -71,8 +71,11 @@ def is_training_forward(name: str) -> bool:
 
 
 class MTracker:
-    """M of every fused-MLP launch in stream order.  The forward / dX kernels run one
-    32-sample tile per wave, so their grid gives M.  dW, its reduction and the input
+    """M of every fused-MLP launch in stream order.  The forward kernels run one
+    32-sample tile per wave, so their grid gives M (rounded up to whole workgroups).  A
+    dX launch takes the M of the newest training forward not yet matched (autograd runs
+    the backwards in reverse forward order; its grid covers whole 256-tile segments, so
+    it gives M only rounded up to 8,192 samples).  dW, its reduction and the input
     gradients follow the backward launch of the same M."""
 
     def __init__(self):
@@ -82,12 +85,12 @@ class MTracker:
     def __call__(self, name: str, grid: int) -> int:
         fam = short(name)
         M = 0
-        if fam in ("mlp_fwd_kernel", "mlp_bwd_kernel", "mlp_fwd_rbm_kernel", "mlp_bwd_rbm_kernel"):
+        if fam in ("mlp_fwd_kernel", "mlp_fwd_rbm_kernel"):
             M = grid // 64 * 32
             if is_training_forward(name):
                 self.fwd_stack.append(M)
-            elif fam in ("mlp_bwd_kernel", "mlp_bwd_rbm_kernel") and self.fwd_stack:
-                self.fwd_stack.pop()
+        elif fam in ("mlp_bwd_kernel", "mlp_bwd_rbm_kernel"):
+            M = self.fwd_stack.pop() if self.fwd_stack else grid // 64 * 32
         elif fam in ("mlp_dw_kernel", "mlp_dw_reduce_kernel", "mlp_dinput_kernel"):
             M = self.last
         self.last = M or self.last
