@@ -2652,34 +2652,20 @@ int launch_fwd(const MlpPlan& p, FwdArgs& a, hipStream_t s) {
     return NR_EARG;
 }
 
-// waves per workgroup of the row-block-major forward for a launch of `tiles` tiles: 8,
-// or 4 when eight-wave workgroups would leave half the 256 CUs idle (a graph-replayed
-// 512-ray step's coarse net: 1024 tiles; 0.068 -> 0.055 ms).  At 3072 tiles (the fine
-// net of that step) four waves lose (0.166 -> 0.176 ms) and the dX chain keeps eight:
-// the coarse backward overlaps the fine forward there and should not take every CU
-// (profiles/r06_rbm_waves.txt).  NR_RBM_WAVES=4|8 forces one (A/B measurements).
-inline int rbm_waves(int64_t tiles) {
-    static const int forced = [] {
-        const char* e = std::getenv("NR_RBM_WAVES");
-        return e ? std::atoi(e) : 0;
-    }();
-    if (forced == 4 || forced == 8) return forced;
-    return ceil_div_ll(tiles, 8) <= 128 ? 4 : 8;
-}
-
 template <int PREC, bool TRAIN>
 int launch_fwd_rbm(const MlpPlan& p, const RbmArgs& a, hipStream_t s) {
-    // every chunk fits a slot (checked at compile time per layer shape)
-    const int w = rbm_waves(a.tiles);
-    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, w))), block(w * 64);
-    const size_t lds = rbm_lds_bytes(p.XB, w);
-#define NR_FWDR(XB_, DB_)                                                                               \
-    if (p.XB == XB_ && p.DB == DB_) {                                                                   \
-        if (w == 4)                                                                                     \
-            hipLaunchKernelGGL((mlp_fwd_rbm_kernel<PREC, XB_, DB_, TRAIN, 4>), grid, block, lds, s, a); \
-        else                                                                                            \
-            hipLaunchKernelGGL((mlp_fwd_rbm_kernel<PREC, XB_, DB_, TRAIN, 8>), grid, block, lds, s, a); \
-        return check_launch("nr_mlp_forward");                                                          \
+    // every chunk fits a slot (checked at compile time per layer shape).  Eight waves per
+    // workgroup at every size: four- and six-wave workgroups for small launches (all CUs
+    // busy, or even rounds) were faster in isolation at 1,024 tiles but slower inside the
+    // graph-replayed 512-ray step, where the coarse backward shares the chip
+    // (profiles/r06_rbm_waves.txt; r04 found the same)
+    constexpr int W = kRbmWaves;
+    const dim3 grid(static_cast<unsigned>(ceil_div_ll(a.tiles, W))), block(W * 64);
+    const size_t lds = rbm_lds_bytes(p.XB, W);
+#define NR_FWDR(XB_, DB_)                                                                           \
+    if (p.XB == XB_ && p.DB == DB_) {                                                               \
+        hipLaunchKernelGGL((mlp_fwd_rbm_kernel<PREC, XB_, DB_, TRAIN, W>), grid, block, lds, s, a); \
+        return check_launch("nr_mlp_forward");                                                      \
     }
     NR_FWDR(2, 1)
 #ifndef NR_MLP_DEV
