@@ -1,5 +1,5 @@
 """GPU: the backward skips 32-sample tiles whose incoming gradient is exactly zero
-(csrc/mlp.hip tile_flags_kernel / tile_list_kernel).
+(csrc/mlp.hip tile_flags_kernel / select_tile).
 
 A sample with sigma == 0 (alpha = w = 0 and ReLU'(0) = 0, reference rendering.py:83) or
 with its transmittance underflowed to 0 (cumprod of 1 - alpha + 1e-10, rendering.py:87-96)
@@ -85,9 +85,10 @@ def test_all_tiles_active_is_bit_identical(precision):
     assert torch.equal(ind[0], ink[0]) and torch.equal(ind[1], ink[1])
 
 
-@pytest.mark.parametrize("precision", ["bf16", "fp16", "fp32"])
-def test_half_the_tiles_inactive(precision):
-    M = 98_304 if precision != "fp32" else 24_576
+@pytest.mark.parametrize("precision,M", [("bf16", 98_304), ("fp16", 98_304), ("fp32", 24_576),
+                                         # ragged: a partial last segment / a partial last tile
+                                         ("bf16", 70_001), ("bf16", 8_225), ("fp32", 9_001)])
+def test_half_the_tiles_inactive(precision, M):
     net = _net(precision, seed=2)
     x, d, gr, gs = _inputs(M, seed=3)
     gr, gs = _zero_tiles(gr, gs, 0.6)
@@ -116,6 +117,25 @@ def test_no_tile_active_gives_zero(precision):
     assert ck == 0
     assert not gk.any() and not gd.any()
     assert not ink[0].any() and not ink[1].any()
+
+
+@pytest.mark.parametrize("M", [33, 1_000, 40_000])
+def test_single_active_tile(M):
+    """One active tile (the last, possibly partial one) among inactive ones: the dX
+    workgroup of its segment runs it with seven idle waves; gradients equal the dense ones
+    (one tile: the same products in the same order)."""
+    net = _net("bf16", seed=4)
+    x, d, gr, gs = _inputs(M, seed=6)
+    T = (M + 31) // 32
+    keep = torch.zeros(M, dtype=torch.bool, device=DEV)
+    keep[(T - 1) * 32:] = True
+    gr, gs = gr * keep[:, None], gs * keep[:, None]
+    gd, ind, cd = _backward(net, x, d, gr, gs, dense=True, inputs=True)
+    gk, ink, ck = _backward(net, x, d, gr, gs, dense=False, inputs=True)
+    assert ck == 1 and cd == T
+    assert torch.equal(ind[0], ink[0]) and torch.equal(ind[1], ink[1])
+    err = (gd - gk).abs().max().item()
+    assert err <= 1e-5 * gd.abs().max().item(), err
 
 
 def test_nan_gradient_keeps_its_tile():
