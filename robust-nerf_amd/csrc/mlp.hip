@@ -1253,10 +1253,11 @@ __device__ __forceinline__ void place_segment(const SegFlags& f, uint32_t before
 //  * every tile active (the dense case: bare-init training, cfg->dense_backward):
 //    workgroup b runs tiles W b .. W b + W - 1, the layout's own order (no lists; dW
 //    takes its identity path on count == tiles);
-//  * otherwise, segment-minor: workgroup b takes part j = b / nseg of segment b % nseg,
-//    i.e. the active tiles W j .. W j + W - 1 of that segment, so the workgroups with
-//    active tiles are dispatched first and spread over every XCD (blocks are dealt to
-//    XCDs round-robin); parts past a segment's count have nothing to do.
+//  * otherwise, segment-minor: workgroup b takes part j = b / nseg of segment
+//    (b - j) mod nseg, i.e. the active tiles W j .. W j + W - 1 of that segment, so the
+//    workgroups with active tiles are dispatched first and spread over every XCD
+//    (blocks are dealt to XCDs round-robin); parts past a segment's count have nothing
+//    to do.
 // Measured (fine bf16 M=786432 dX, profiles/r06_tile_map_ab.txt): segment-minor in the
 // dense case costs ~7 % at M=786432 and ~20 % at 262144 (locality), segment-major in
 // the skipping case 1.67x at 37 % active.
@@ -1273,8 +1274,12 @@ __device__ __forceinline__ TileSel select_tile(const uint8_t* __restrict__ flags
     const int lane = threadIdx.x & 63;
     const int64_t b = blockIdx.x;
     TileSel t;
-    t.seg = b % nseg;
+    // skipping form: part-major over the segments (the parts with active tiles go first),
+    // the segment rotated by the part, so that one segment's parts land on different
+    // XCDs (b % 8) even when nseg is a multiple of 8: segments whose counts differ (a
+    // trained field's rays hit or miss as a whole) then load every XCD alike
     const int part = static_cast<int>(b / nseg);
+    t.seg = (b % nseg + nseg - part % nseg) % nseg;
     // every load first (one round trip): the segment's flag word and the block counts,
     // one uint4 (a segment's four blocks) per lane and 64 segments
     static_assert(BPS == 4, "a segment's block counts are one uint4");

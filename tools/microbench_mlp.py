@@ -19,9 +19,20 @@ def bench(prec, M, reps=int(__import__("os").environ.get("MB_REPS", "20"))):
     grgb = torch.randn(M, 3, device="cuda"); gs = torch.randn(M, 1, device="cuda")
     # MB_ACTIVE=f: zero the incoming gradient of all but a fraction f of the 32-sample tiles
     # (the trained-state regime: the backward then runs on the active tiles only)
+    # MB_PATTERN=rays: whole rays of MB_TPR tiles (default 6: 192 samples) are active in
+    # their tiles 1..MB_TPR-1 with probability f / ((MB_TPR-1)/MB_TPR) (a trained field's
+    # shape: rays that miss have no active tile, rays that hit one run of them)
     f = float(__import__("os").environ.get("MB_ACTIVE", "1"))
     if f < 1:
-        keep = (torch.rand((M + 31) // 32, device="cuda") < f).repeat_interleave(32)[:M]
+        T = (M + 31) // 32
+        if __import__("os").environ.get("MB_PATTERN") == "rays":
+            tpr = int(__import__("os").environ.get("MB_TPR", "6"))
+            hit = torch.rand((T + tpr - 1) // tpr, device="cuda") < f * tpr / (tpr - 1)
+            run = torch.ones(tpr, dtype=torch.bool, device="cuda"); run[0] = False
+            tk = (hit[:, None] & run[None, :]).reshape(-1)[:T]
+        else:
+            tk = torch.rand(T, device="cuda") < f
+        keep = tk.repeat_interleave(32)[:M]
         grgb *= keep[:, None]; gs *= keep[:, None]
     gflat = torch.empty_like(flat)
     P = _hip.ptr
