@@ -24,7 +24,6 @@
 // rebuilds sample-major operands with the gfx950 transpose read
 // ds_read_b64_tr_b16 (bf16) or strided ds_read_b32 (fp32).
 #include <cmath>
-#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <utility>
