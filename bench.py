@@ -95,7 +95,8 @@ def rocprof_summary(prec: str):
                 # same-source measurement
                 if r.get("source_hash") != want or r.get("hash_overridden"):
                     break
-                if r.get("M_samples") and r.get("precision", prec) == prec:
+                # the slab reduction is not precision-templated: its rows carry no precision
+                if r.get("M_samples") and r.get("precision") in (prec, ""):
                     rows[(r["kernel"], int(r["M_samples"]))] = r
         if rows:
             return rows, f"profiles/{f.name}"

@@ -24,7 +24,7 @@ def _summary_rows(name="r06_kernel_summary.csv"):
     rows = {}
     with open(ROOT / "profiles" / name) as f:
         for r in csv.DictReader(f):
-            if r.get("M_samples") and r.get("precision") == "bf16":
+            if r.get("M_samples") and r.get("precision") in ("bf16", ""):
                 rows[(r["kernel"], int(r["M_samples"]))] = r
     return rows
 
@@ -54,6 +54,20 @@ def test_rocprof_basis_agrees_with_headline():
     # one step's fused-MLP launches fit in the recorded step of the same tree
     rec = json.loads((ROOT / "profiles" / "r06_bench_full.json").read_text().strip().splitlines()[-1])
     assert sum(v["ms"] for v in ktab.values()) <= rec["ms_per_step"]
+
+
+def test_committed_summary_covers_every_entry():
+    """bench.rocprof_summary picks up every fused-MLP key of the step from the committed
+    summary, the precision-independent slab reduction included, when its source hash is
+    this tree's."""
+    rows, src = bench.rocprof_summary("bf16")
+    if src is None:
+        import pytest
+        pytest.skip("no committed kernel summary of this tree's sources (re-profile after a csrc change)")
+    keys = {(k, M) for k, M in rows}
+    for entry, kerns in bench.KERNEL_OF.items():
+        for M in (262144, 786432):
+            assert any((k, M) in keys for k in kerns), (entry, M)
 
 
 def test_bracketed_entries_carry_no_fraction():
