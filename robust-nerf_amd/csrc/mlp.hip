@@ -1260,6 +1260,8 @@ __device__ __forceinline__ void place_segment(const SegFlags& f, uint32_t before
 // Measured (fine bf16 M=786432 dX, profiles/r06_tile_map_ab.txt): segment-minor in the
 // dense case costs ~7 % at M=786432 and ~20 % at 262144 (locality), segment-major in
 // the skipping case 1.67x at 37 % active.
+constexpr int64_t kDenseCheckSegs = 1024;  // launches up to 262,144 tiles check for "all active"
+
 struct TileSel {
     SegFlags sf;
     int64_t seg, tile;
@@ -1280,17 +1282,22 @@ __device__ __forceinline__ TileSel select_tile(const uint8_t* __restrict__ flags
     const int part = static_cast<int>(b / nseg);
     t.seg = (b % nseg + nseg - part % nseg) % nseg;
     // every load first (one round trip): the segment's flag word and the block counts,
-    // one uint4 (a segment's four blocks) per lane and 64 segments
+    // one uint4 (a segment's four blocks) per lane and 64 segments.  Past
+    // kDenseCheckSegs segments (M > 8.4M samples) reading every count in every workgroup
+    // would grow with M^2: such launches take the skipping form, which is right for any
+    // flags, and only the leaders read the counts before their segment
     static_assert(BPS == 4, "a segment's block counts are one uint4");
+    const bool check = nseg <= kDenseCheckSegs;  // launch-uniform
+    const int64_t lim = check ? nseg : (part == 0 && wv == 0 ? t.seg : 0);
     const uint32_t word = seg_flag_word(flags, t.seg);
     const uint4* __restrict__ bc4 = reinterpret_cast<const uint4*>(blk_count);
     uint32_t all = 0, before = 0;
-    for (int64_t s0 = 0; s0 < nseg; s0 += 4 * 64) {
+    for (int64_t s0 = 0; s0 < lim; s0 += 4 * 64) {
         uint4 c[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t sg = s0 + i * 64 + lane;
-            c[i] = sg < nseg ? bc4[sg] : uint4{0u, 0u, 0u, 0u};
+            c[i] = sg < lim ? bc4[sg] : uint4{0u, 0u, 0u, 0u};
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1306,7 +1313,7 @@ __device__ __forceinline__ TileSel select_tile(const uint8_t* __restrict__ flags
         before += __shfl_xor(before, d);
     }
     t.before = __builtin_amdgcn_readfirstlane(before);
-    t.dense = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(all)) == tiles;
+    t.dense = check && static_cast<int64_t>(__builtin_amdgcn_readfirstlane(all)) == tiles;
     if (t.dense) {
         const int64_t first = b * W;
         t.tile = first + wv;

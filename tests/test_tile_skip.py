@@ -138,6 +138,26 @@ def test_single_active_tile(M):
     assert err <= 1e-5 * gd.abs().max().item(), err
 
 
+def test_launch_past_the_dense_check():
+    """Past kDenseCheckSegs (1,024) segments of 256 tiles (M > 8,388,608 samples) the dX
+    workgroups skip the all-active check, which would read every block count in every
+    workgroup, and always take the segment-minor form (leaders alone read the counts
+    before their segment).  Both the dense form (every tile flagged) and the skipping one
+    run that way: same input gradients bit for bit, dW to summation order, right count."""
+    M = 1_025 * 8_192 + 77  # 1,026 segments, a ragged last one
+    T = (M + 31) // 32
+    net = _net("bf16", seed=8)
+    x, d, gr, gs = _inputs(M, seed=9)
+    gr, gs = _zero_tiles(gr, gs, 0.5, seed=10)
+    want = _expected_active(gr, gs)
+    gd, ind, cd = _backward(net, x, d, gr, gs, dense=True, inputs=True)
+    gk, ink, ck = _backward(net, x, d, gr, gs, dense=False, inputs=True)
+    assert cd == T and ck == want
+    assert torch.equal(ind[0], ink[0]) and torch.equal(ind[1], ink[1])
+    rel = ((gd - gk).norm() / gd.norm()).item()
+    assert rel < 1e-5, rel
+
+
 def test_nan_gradient_keeps_its_tile():
     """A NaN incoming gradient is not zero: its tile runs (and the NaN reaches dW)."""
     M = 3_200
