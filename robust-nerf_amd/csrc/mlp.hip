@@ -1810,7 +1810,7 @@ constexpr int kTileFlagThreads = 256;  // 4 waves x 16 tiles: one 64-tile block 
 
 __global__ __launch_bounds__(kTileFlagThreads) void tile_flags_kernel(const float* __restrict__ g_rgb,
                                                                       const float* __restrict__ g_sigma, int64_t M,
-                                                                      int64_t tiles, int dense,
+                                                                      int dense,
                                                                       uint8_t* __restrict__ flags,
                                                                       uint32_t* __restrict__ blk_count) {
     __shared__ uint32_t wcnt[kTileFlagThreads / 64];
@@ -3097,7 +3097,7 @@ int nr_mlp_backward_dx(const NrMlpConfig* cfg, const void* packed, const float* 
     uint32_t* dwlist = reinterpret_cast<uint32_t*>(wsb + z.dwlist_off);
     uint32_t* tcount = reinterpret_cast<uint32_t*>(wsb + z.count_off);
     hipLaunchKernelGGL(tile_flags_kernel, dim3(static_cast<unsigned>(z.nseg * (kSegTiles / 64))),
-                       dim3(kTileFlagThreads), 0, s, g_rgb, g_sigma, M, z.tiles, p.dense_bwd, tflags, blkcnt);
+                       dim3(kTileFlagThreads), 0, s, g_rgb, g_sigma, M, p.dense_bwd, tflags, blkcnt);
     NR_LAUNCH_CHECK("nr_mlp_backward_dx (tile flags)");
     BwdArgs b;
     std::memset(&b, 0, sizeof(b));
