@@ -1832,7 +1832,7 @@ __global__ __launch_bounds__(kTileFlagThreads) void tile_flags_kernel(const floa
         }
         nz[it] = v;
     }
-    uint32_t mask = 0;  // bit k: tile tw + k is active (wave-uniform); tiles past `tiles`: 0
+    uint32_t mask = 0;  // bit k: tile tw + k is active (wave-uniform); tiles past the last sample: 0
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
         const uint64_t b = __ballot(nz[it]);
