@@ -7,7 +7,7 @@
 // order, as torch's CPU cumsum); u = linspace(0,1,Ns) if det else the caller's
 // uniforms; idx = searchsorted(cdf, u, right=True); below/above clamped; the
 // `denom < 1e-5 -> 1` rule; s = b0 + (u-c0)/denom * (b1-b0).  The hierarchical
-// form then sorts cat(z_coarse, s) — here a bitonic sort in the wave's LDS, whose
+// form then sorts cat(z_coarse, s) — here a bitonic sort in the wave's registers, whose
 // output values equal torch.sort's whatever the order of u.
 #include "common.hpp"
 
@@ -103,6 +103,46 @@ __global__ void sample_pdf_kernel(const float* bins_g, const float* w_g, const f
     }
 }
 
+// Bitonic sort (ascending) of R * 64 values held R per lane (element 64 i + lane in
+// register i), fully unrolled: strides below 64 exchange across lanes (__shfl_xor),
+// strides of 64 and more between a lane's own registers.  Compare-exchange is
+// fminf / fmaxf, so the output is the sorted multiset whatever the input order (equal
+// values are interchangeable: only values leave the sort, as in torch.sort(...)[0]).
+template <int R, int K, int J>
+__device__ __forceinline__ void bitonic_step(float (&v)[R], int lane) {
+    if constexpr (J >= 64) {
+        constexpr int M = J / 64;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            if ((i & M) == 0) {
+                const bool asc = ((i * 64) & K) == 0;  // K > J >= 64: the lane bits do not matter
+                const float x = v[i], y = v[i ^ M];
+                v[i] = asc ? fminf(x, y) : fmaxf(x, y);
+                v[i ^ M] = asc ? fmaxf(x, y) : fminf(x, y);
+            }
+        }
+    } else {
+        const bool lo = (lane & J) == 0;  // the lower element of its pair
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const bool asc = K >= 64 ? ((i * 64) & K) == 0 : (lane & K) == 0;
+            const float y = __shfl_xor(v[i], J);
+            v[i] = lo == asc ? fminf(v[i], y) : fmaxf(v[i], y);
+        }
+    }
+    if constexpr (J > 1) bitonic_step<R, K, J / 2>(v, lane);
+}
+template <int R, int K = 2>
+__device__ __forceinline__ void bitonic_sort(float (&v)[R], int lane) {
+    bitonic_step<R, K, K / 2>(v, lane);
+    if constexpr (K < R * 64) bitonic_sort<R, K * 2>(v, lane);
+}
+
+// One wave per ray.  The wave's T = Nc + Nf values (coarse z, then the inverse-CDF
+// samples) live in registers, R = P / 64 per lane for the padded length P (+inf past T),
+// and are sorted there: the LDS form (v1) spent 11-14 us of 19-26 in its 36 LDS
+// exchange rounds (tools/proto_sample_hier.hip).  LDS holds only bins, cdf and weights.
+template <int R>
 __global__ void sample_hier_kernel(const float* ro, const float* rd, const float* zc_g, const float* wc_g,
                                    const float* u_g, int B, int Nc, int Nf, float* zf_out, float* pts_out,
                                    float* vd_out) {
@@ -110,52 +150,46 @@ __global__ void sample_hier_kernel(const float* ro, const float* rd, const float
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int b = blockIdx.x * kRaysPerBlock + wv;
     const int Nb = Nc - 1, T = Nc + Nf;
-    int P2 = 1;  // the sort's padded length (below)
-    while (P2 < T) P2 <<= 1;
-    float* bins = smem + wv * (3 * Nb + P2);
+    float* bins = smem + wv * (3 * Nb);
     float* cdf = bins + Nb;
     float* wbuf = cdf + Nb;
-    float* uni = wbuf + Nb;
     const bool live = b < B;
     const int64_t zb = static_cast<int64_t>(b) * Nc;
+    float v[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) v[i] = 0.f;
     if (live) {
-        for (int i = lane; i < Nc; i += 64) uni[i] = zc_g[zb + i];
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            if (i * 64 + lane < Nc) v[i] = zc_g[zb + i * 64 + lane];
         for (int i = lane; i < Nc - 2; i += 64) wbuf[i] = wc_g[zb + 1 + i];  // weights[..., 1:-1]
-    }
-    __syncthreads();
-    if (live) {
-        for (int i = lane; i < Nb; i += 64) bins[i] = 0.5f * (uni[i + 1] + uni[i]);  // z_vals_mid
-        build_cdf(wbuf, cdf, Nb, lane);
-    }
-    __syncthreads();
-    if (live) {
-        for (int j = lane; j < Nf; j += 64) {
-            const float u = u_g ? u_g[static_cast<int64_t>(b) * Nf + j] : linspace01(Nf, j);
-            uni[Nc + j] = invert_cdf(cdf, bins, Nb, u);
+        // z_vals_mid: z[e + 1] from the next lane (lane 63: lane 0 of the next register)
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const float nxt = __shfl(v[i], (lane + 1) & 63);
+            const float wrap = __shfl(v[i + 1 < R ? i + 1 : i], 0);
+            const int e = i * 64 + lane;
+            if (e < Nb) bins[e] = 0.5f * ((lane == 63 ? wrap : nxt) + v[i]);
         }
     }
+    __syncthreads();
+    if (live) build_cdf(wbuf, cdf, Nb, lane);
     __syncthreads();
     if (!live) return;
-    // bitonic sort of uni[0..T), padded with +inf to P = 2^ceil(log2 T), in the wave's
-    // LDS (only the values leave the sort, as in torch.sort(...)[0], so the order among
-    // equal values cannot show).  An all-pairs rank sort cost T^2 compares per ray.
-    const int P = P2;
-    for (int e = T + lane; e < P; e += 64) uni[e] = __builtin_inff();
-    wave_lds_sync();
-    for (int k = 2; k <= P; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int t = lane; t < (P >> 1); t += 64) {
-                const int lo = ((t & ~(j - 1)) << 1) | (t & (j - 1)), hi = lo + j;
-                const float x = uni[lo], y = uni[hi];
-                const bool swap = (lo & k) == 0 ? (x > y) : (x < y);
-                if (swap) {
-                    uni[lo] = y;
-                    uni[hi] = x;
-                }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int e = i * 64 + lane;
+        if (e >= Nc) {
+            if (e < T) {
+                const int j = e - Nc;
+                const float u = u_g ? u_g[static_cast<int64_t>(b) * Nf + j] : linspace01(Nf, j);
+                v[i] = invert_cdf(cdf, bins, Nb, u);
+            } else {
+                v[i] = __builtin_inff();
             }
-            wave_lds_sync();
         }
     }
+    bitonic_sort<R>(v, lane);
     const int64_t ob = static_cast<int64_t>(b) * T;
     float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 0.f, dz = 0.f;
     if (pts_out || vd_out) {
@@ -167,19 +201,22 @@ __global__ void sample_hier_kernel(const float* ro, const float* rd, const float
         const float dn = norm3(dx, dy, dz);
         vx = dx / dn, vy = dy / dn, vz = dz / dn;
     }
-    for (int e = lane; e < T; e += 64) {
-        const float v = uni[e];
-        const int64_t o = ob + e;
-        zf_out[o] = v;
-        if (pts_out) {
-            pts_out[3 * o] = ox + dx * v;
-            pts_out[3 * o + 1] = oy + dy * v;
-            pts_out[3 * o + 2] = oz + dz * v;
-        }
-        if (vd_out) {
-            vd_out[3 * o] = vx;
-            vd_out[3 * o + 1] = vy;
-            vd_out[3 * o + 2] = vz;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int e = i * 64 + lane;
+        if (e < T) {
+            const int64_t o = ob + e;
+            zf_out[o] = v[i];
+            if (pts_out) {
+                pts_out[3 * o] = ox + dx * v[i];
+                pts_out[3 * o + 1] = oy + dy * v[i];
+                pts_out[3 * o + 2] = oz + dz * v[i];
+            }
+            if (vd_out) {
+                vd_out[3 * o] = vx;
+                vd_out[3 * o + 1] = vy;
+                vd_out[3 * o + 2] = vz;
+            }
         }
     }
 }
@@ -209,12 +246,17 @@ int nr_sample_hierarchical(const float* ro, const float* rd, const float* zc, co
     NR_REQUIRE(Nc + Nf <= 64 * kMaxPerLane, "nr_sample_hierarchical: Nc+Nf=%d exceeds %d", Nc + Nf,
                64 * kMaxPerLane);
     if (B == 0) return NR_OK;
-    int P2 = 1;  // the kernel's sort pads Nc + Nf to a power of two
+    int P2 = 64;  // the kernel's sort pads Nc + Nf to a power of two, at least one wave
     while (P2 < Nc + Nf) P2 <<= 1;
-    const size_t lds = sizeof(float) * kRaysPerBlock * (3 * (Nc - 1) + P2);
+    const size_t lds = sizeof(float) * kRaysPerBlock * 3 * (Nc - 1);
     const dim3 grid(ceil_div(B, kRaysPerBlock)), block(64 * kRaysPerBlock);
     const hipStream_t st = static_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(sample_hier_kernel, grid, block, lds, st, ro, rd, zc, wc, u, B, Nc, Nf, zf, pts, viewdirs);
+    switch (P2 / 64) {  // values per lane
+        case 1: hipLaunchKernelGGL(sample_hier_kernel<1>, grid, block, lds, st, ro, rd, zc, wc, u, B, Nc, Nf, zf, pts, viewdirs); break;
+        case 2: hipLaunchKernelGGL(sample_hier_kernel<2>, grid, block, lds, st, ro, rd, zc, wc, u, B, Nc, Nf, zf, pts, viewdirs); break;
+        case 4: hipLaunchKernelGGL(sample_hier_kernel<4>, grid, block, lds, st, ro, rd, zc, wc, u, B, Nc, Nf, zf, pts, viewdirs); break;
+        default: hipLaunchKernelGGL(sample_hier_kernel<8>, grid, block, lds, st, ro, rd, zc, wc, u, B, Nc, Nf, zf, pts, viewdirs); break;
+    }
     NR_LAUNCH_CHECK("nr_sample_hierarchical");
     return NR_OK;
 }
