@@ -259,15 +259,18 @@ class Trainer:
             main = torch.cuda.current_stream(rays_o.device)
             loss_f = out["loss_fine"]
             loss_c = early["loss_c"].detach()
-            # the summed value on the coarse stream, beside the fine backward (the backward
-            # already ran for loss_c; d(loss_c + loss_f) = d loss_f for the fine net)
-            cs.wait_stream(main)
             lf = loss_f.detach()
+            fine_done = main.record_event()
+            loss_f.backward(ops.unit_grad(rays_o.device))
+            # the summed value on the coarse stream, beside the fine backward (the backward
+            # already ran for loss_c; d(loss_c + loss_f) = d loss_f for the fine net).
+            # Captured after the fine backward, so that a graph replay keeps the fine
+            # chain on one hardware queue (a hop between queues costs ~10 us)
+            cs.wait_event(fine_done)
             lf.record_stream(cs)
             with torch.cuda.stream(cs):
                 loss = loss_c + lf
             loss.record_stream(main)
-            loss_f.backward(ops.unit_grad(rays_o.device))
             main.wait_stream(cs)  # join the coarse chain
             metrics = {"loss_coarse": loss_c, "loss_fine": lf}
         else:
